@@ -1,0 +1,845 @@
+// render.hip — the MI355X (gfx950) per-pixel path-trace kernel and its launchers.
+//
+// Replaces __global__ Kernel / RenderInit / RandInit and the extern "C" launchers of
+// CudaRayTracer/src/Cuda/Kernel.cu:102-204.  Design:
+//   * one lane per pixel; a 256-thread workgroup renders a 16×16 pixel tile, each wave64 an 8×8 sub-tile
+//     so the primary rays of a wave are coherent;
+//   * the sample loop (Kernel.cu:137) and the bounce loop of color() (Kernel.cu:39) are flattened into
+//     ONE per-lane ray loop: a lane whose path ends starts its next sample at once instead of idling until
+//     the slowest lane of the wave finishes its path.  The per-lane order of RNG draws, and so the result,
+//     is unchanged;
+//   * closest hit through a binary BVH whose child boxes sit in the parent node (one 64-B node fetch
+//     tests two boxes), near-child-first traversal with a short per-lane stack; the scene tables are
+//     read through the L1/L2 or staged in LDS (template choice);
+//   * the cuRAND XORWOW state (Kernel.cu:123, 149) lives in VGPRs for the whole frame: 24 B loaded and
+//     24 B stored per pixel;
+//   * no MFMA: there is no dense contraction on this path.
+//
+// Arithmetic contract (bit-for-bit with oracle/rt_oracle.c): this file is compiled with
+// -ffp-contract=off; every +,-,*,/ and sqrtf of the reference expressions is one correctly rounded
+// binary32 operation, in the reference's association order.  Only the slab test of the BVH boxes uses
+// explicit FMAs: boxes are padded outward on the host, so box culling never rejects a primitive the
+// exact test accepts and the closest hit is decided by the exact primitive tests alone.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+#include "rt_internal.h"
+#include "rt_scene_device.h"
+
+namespace rt {
+namespace dev {
+
+// ---------------------------------------------------------------------------------------------------
+// Vec3 algebra (Utils/Math.cuh:16-229), one IEEE op per component, reference association order.
+// ---------------------------------------------------------------------------------------------------
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 scale(float t, f3 v) { return mk(t * v.x, t * v.y, t * v.z); }
+__device__ __forceinline__ f3 divs(f3 v, float t) { return mk(v.x / t, v.y / t, v.z / t); }
+__device__ __forceinline__ f3 neg(f3 v) { return mk(-v.x, -v.y, -v.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+__device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, length(v)); }
+__device__ __forceinline__ f3 normalize(f3 v) {
+    float inv = 1.0f / sqrtf(dot(v, v));
+    return scale(inv, v);
+}
+__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }
+__device__ __forceinline__ float clampf(float x, float a, float b) { return (x < a) ? a : ((x > b) ? b : x); }
+__device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
+
+// ---------------------------------------------------------------------------------------------------
+// cuRAND XORWOW (curand_kernel.h: curand(), _curand_uniform) in registers.
+// ---------------------------------------------------------------------------------------------------
+struct Rng {
+    uint32_t d, v0, v1, v2, v3, v4;
+};
+__device__ __forceinline__ float uniform(Rng& s) {
+    uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1;
+    s.v1 = s.v2;
+    s.v2 = s.v3;
+    s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    uint32_t x = s.v4 + s.d;
+    return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
+}
+
+// RandomInUnitSphere (Math.cuh:252-260) with Random() (Math.cuh:231-234).  rtl: the components of
+// Vec3(ξa, ξb, ξc) are filled right to left (z = first draw), as the survey's g++ build evaluated it.
+__device__ __forceinline__ f3 random_in_unit_sphere(Rng& s, bool rtl) {
+    f3 p;
+    do {
+        float a = uniform(s);
+        float b = uniform(s);
+        float c = uniform(s);
+        f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
+        p = sub(scale(2.0f, r), mk(1.0f, 1.0f, 1.0f));
+    } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
+    return p;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Kernel parameters (by value; everything launch-uniform precomputed on the host with the same
+// binary32 operations the reference performs per thread).
+// ---------------------------------------------------------------------------------------------------
+struct KParams {
+    const float4* nodes;
+    const float4* prims;
+    const float4* mats;
+    const int4* imgs;
+    const uint8_t* texels;
+    uint32_t* pos;
+    float4* radiance;
+    float4* accum;
+    uint32_t* state;  // 12 words per rt_curand_state
+    unsigned long long* counters;
+    uint32_t num_nodes, num_prims;
+    uint32_t width, height, spp, max_depth, flags;
+    uint32_t band_rows, num_ranks, rank, local_rows;
+    uint32_t tiles_x;
+    uint32_t grid_w, grid_h;  // pixels rendered: x < grid_w, global row < grid_h
+    uint32_t rius_rtl;
+    float width_f, cx, cy;
+    float near_plane, far_plane;
+    float origin[3], up[3], right[3];
+    float fov_fwd[3];  // inputs.fov * forwardV           (Kernel.cu:142)
+    float k10_fwd[3];  // (1.0f / inputs.fov * 10.0f) * forwardV (Kernel.cu:143)
+    float bg0[3], bg1[3];
+};
+
+constexpr int kStackMax = 64;
+constexpr int kBlock = 256;
+constexpr int kLdsStackDepth = 24;
+
+enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_HYBRID = 2 };
+
+// Per-lane traversal stacks -------------------------------------------------------------------------
+struct ScratchStack {
+    int s[kStackMax];
+    int n;
+    __device__ __forceinline__ void init(uint32_t*) { n = 0; }
+    __device__ __forceinline__ void push(int v) { s[n++] = v; }
+    __device__ __forceinline__ int pop() { return s[--n]; }
+    __device__ __forceinline__ bool empty() const { return n == 0; }
+};
+
+struct LdsStack {  // [depth][256] layout: lane-consecutive, bank-conflict free
+    uint32_t* base;
+    int n;
+    __device__ __forceinline__ void init(uint32_t* lds) { base = lds + threadIdx.x; n = 0; }
+    __device__ __forceinline__ void push(int v) { base[(n++) * kBlock] = (uint32_t)v; }
+    __device__ __forceinline__ int pop() { return (int)base[(--n) * kBlock]; }
+    __device__ __forceinline__ bool empty() const { return n == 0; }
+};
+
+struct HybridStack {  // top 4 entries in VGPRs, deeper entries in scratch
+    int r0, r1, r2, r3;
+    int spill[kStackMax];
+    int n;
+    __device__ __forceinline__ void init(uint32_t*) { n = 0; }
+    __device__ __forceinline__ void push(int v) {
+        if (n >= 4) spill[n - 4] = r3;
+        r3 = r2; r2 = r1; r1 = r0; r0 = v;
+        n++;
+    }
+    __device__ __forceinline__ int pop() {
+        int v = r0;
+        r0 = r1; r1 = r2; r2 = r3;
+        n--;
+        if (n >= 4) r3 = spill[n - 4];
+        return v;
+    }
+    __device__ __forceinline__ bool empty() const { return n == 0; }
+};
+
+template <int K> struct StackOf;
+template <> struct StackOf<STACK_SCRATCH> { using T = ScratchStack; };
+template <> struct StackOf<STACK_LDS> { using T = LdsStack; };
+template <> struct StackOf<STACK_HYBRID> { using T = HybridStack; };
+
+struct Counts {
+    uint32_t rays, boxes, prims, primary;
+};
+
+constexpr int kEmpty = (int)0x80000000;
+constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX, rec) (Kernel.cu:40)
+
+// Closest hit (BVHNode::Hit, Hittable.cuh:387-439, and the primitive tests of PerformHit :470-485).
+// Returns the primitive index (BVH order) or -1, and the hit distance in t_best.
+template <int STACK, bool COUNT>
+__device__ __forceinline__ int trace(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                                     uint32_t num_nodes, f3 o, f3 d, float a_dd, float& t_best,
+                                     uint32_t* lds_stack, Counts& cnt) {
+    t_best = FLT_MAX;
+    int hit = -1;
+    if (num_nodes == 0) return -1;
+    // Slab test in fma form, t = lo·invd − o·invd, on boxes padded outward on the host.  A direction
+    // component that is exactly 0 (e.g. a Lambertian bounce whose tiny offset vanished against a large
+    // hit coordinate, (p + n + q) − p) would give inf − inf; clamping 1/d to ±1e20 keeps the test
+    // conservative: the position error of the fma form (~ulp of the coordinates) stays far below the
+    // 1e-5-relative box padding.
+    const f3 invd = mk(fminf(fmaxf(1.0f / d.x, -1e20f), 1e20f), fminf(fmaxf(1.0f / d.y, -1e20f), 1e20f),
+                       fminf(fmaxf(1.0f / d.z, -1e20f), 1e20f));
+    const float oix = o.x * invd.x, oiy = o.y * invd.y, oiz = o.z * invd.z;
+    typename StackOf<STACK>::T stack;
+    stack.init(lds_stack);
+    int node = 0;
+    while (true) {
+        while (node >= 0) {
+            const float4 n0 = nodes[4 * node + 0];
+            const float4 n1 = nodes[4 * node + 1];
+            const float4 n2 = nodes[4 * node + 2];
+            const float4 n3 = nodes[4 * node + 3];
+            const float a0 = __builtin_fmaf(n0.x, invd.x, -oix), a1 = __builtin_fmaf(n0.y, invd.x, -oix);
+            const float a2 = __builtin_fmaf(n0.z, invd.y, -oiy), a3 = __builtin_fmaf(n0.w, invd.y, -oiy);
+            const float a4 = __builtin_fmaf(n2.x, invd.z, -oiz), a5 = __builtin_fmaf(n2.y, invd.z, -oiz);
+            const float b0 = __builtin_fmaf(n1.x, invd.x, -oix), b1 = __builtin_fmaf(n1.y, invd.x, -oix);
+            const float b2 = __builtin_fmaf(n1.z, invd.y, -oiy), b3 = __builtin_fmaf(n1.w, invd.y, -oiy);
+            const float b4 = __builtin_fmaf(n2.z, invd.z, -oiz), b5 = __builtin_fmaf(n2.w, invd.z, -oiz);
+            const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+            const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+            const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+            const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+            if (COUNT) cnt.boxes += 2;
+            const bool h0 = c0min <= c0max;
+            const bool h1 = c1min <= c1max;
+            const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+            if (h0 && h1) {
+                const bool swap = c1min < c0min;
+                node = swap ? ch1 : ch0;
+                stack.push(swap ? ch0 : ch1);
+            } else if (h0 | h1) {
+                node = h0 ? ch0 : ch1;
+            } else {
+                node = stack.empty() ? kEmpty : stack.pop();
+            }
+        }
+        if (node == kEmpty) break;
+        // leaf: primitives [first, first + count)
+        const uint32_t leaf = ~(uint32_t)node;
+        const uint32_t first = leaf >> 4, count = leaf & 15u;
+        for (uint32_t i = first; i < first + count; i++) {
+            const float4 p0 = prims[2 * i + 0];
+            const float4 p1 = prims[2 * i + 1];
+            const uint32_t type = __float_as_uint(p1.w) & 15u;
+            if (COUNT) cnt.prims++;
+            if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                const f3 oc = sub(o, xyz(p0));
+                const float b = dot(oc, d);
+                const float c = dot(oc, oc) - p1.x;  // p1.x = radius · radius
+                const float disc = b * b - a_dd * c;
+                if (disc > 0) {
+                    const float sq = sqrtf(disc);
+                    float t = (-b - sq) / a_dd;
+                    if (t < t_best && t > kTmin) {
+                        t_best = t;
+                        hit = (int)i;
+                    } else {
+                        t = (-b + sq) / a_dd;
+                        if (t < t_best && t > kTmin) {
+                            t_best = t;
+                            hit = (int)i;
+                        }
+                    }
+                }
+            } else {  // XY/XZ/YZRect::Hit (Hittable.cuh:140-169, 196-225, 252-281)
+                const float ok = type == RT_XYRECT ? o.z : (type == RT_XZRECT ? o.y : o.x);
+                const float dk = type == RT_XYRECT ? d.z : (type == RT_XZRECT ? d.y : d.x);
+                const float t = (p0.x - ok) * (1.0f / dk);
+                if (!(t < kTmin || t > t_best)) {
+                    const float oa = type == RT_YZRECT ? o.y : o.x, da = type == RT_YZRECT ? d.y : d.x;
+                    const float ob = type == RT_XYRECT ? o.y : o.z, db = type == RT_XYRECT ? d.y : d.z;
+                    const float x = oa + t * da;
+                    const float y = ob + t * db;
+                    if (!(x < p0.y || x > p0.z || y < p0.w || y > p1.x)) {
+                        t_best = t;
+                        hit = (int)i;
+                    }
+                }
+            }
+        }
+        if (stack.empty()) break;
+        node = stack.pop();
+    }
+    return hit;
+}
+
+// Texture::value (Texture.cuh:42-45, 58-67, 83-105)
+__device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, const float4& m2, uint32_t tex_type,
+                                            float u, float v, f3 p, const int4* __restrict__ imgs,
+                                            const uint8_t* __restrict__ texels) {
+    if (tex_type == RT_CONSTANT) return xyz(m1);
+    if (tex_type == RT_CHECKER) {
+        const float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+        return sines < 0 ? xyz(m1) : xyz(m2);
+    }
+    if (tex_type == RT_IMAGE) {
+        const int img = __float_as_int(m0.w);
+        const int4 im = imgs[img];
+        if (im.x < 0) return mk(0.0f, 1.0f, 1.0f);  // data == nullptr
+        u = clampf(u, 0.0f, 1.0f);
+        v = 1.0f - clampf(v, 0.0f, 1.0f);
+        int i = (int)(u * (float)im.y);
+        int j = (int)(v * (float)im.z);
+        if (i >= im.y) i = im.y - 1;
+        if (j >= im.z) j = im.z - 1;
+        const float color_scale = 1.0f / 255.0f;
+        const uint8_t* px = texels + im.x + (size_t)j * (size_t)(3 * im.y) + (size_t)i * 3;
+        return mk(color_scale * (float)px[0], color_scale * (float)px[1], color_scale * (float)px[2]);
+    }
+    return mk(0.0f, 0.0f, 0.0f);
+}
+
+__device__ __forceinline__ uint32_t f2u8(float f) { return f != f ? 0u : (uint32_t)(int)f; }
+
+// RgbToInt (Kernel.cu:12-19)
+__device__ __forceinline__ uint32_t rgb_to_int(float r, float g, float b) {
+    r = clampf(r, 0.0f, 255.0f);
+    g = clampf(g, 0.0f, 255.0f);
+    b = clampf(b, 0.0f, 255.0f);
+    return (255u << 24) | (f2u8(b) << 16) | (f2u8(g) << 8) | f2u8(r);
+}
+
+__device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t local_row) {
+    const uint32_t band = local_row / P.band_rows, within = local_row - band * P.band_rows;
+    return (band * P.num_ranks + P.rank) * P.band_rows + within;
+}
+
+// Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop.
+template <bool SCENE_LDS, int STACK, bool COUNT_TESTS>
+__global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
+    extern __shared__ float4 lds[];
+    const float4* nodes = P.nodes;
+    const float4* prims = P.prims;
+    uint32_t* lds_stack = nullptr;
+    if constexpr (SCENE_LDS) {
+        const uint32_t nn = P.num_nodes * 4, np = P.num_prims * 2;
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlock) lds[i] = P.nodes[i];
+        for (uint32_t i = threadIdx.x; i < np; i += kBlock) lds[nn + i] = P.prims[i];
+        __syncthreads();
+        nodes = lds;
+        prims = lds + nn;
+        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)(lds + nn + np);
+    } else {
+        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)lds;
+    }
+
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t bx = blockIdx.x % P.tiles_x, by = blockIdx.x / P.tiles_x;
+    const uint32_t x = bx * 16 + (wave & 1u) * 8 + (lane & 7u);
+    const uint32_t ly = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (x >= P.width || ly >= P.local_rows) return;
+    const uint32_t g = global_row(P, ly);
+    if (x >= P.grid_w || g >= P.grid_h) return;  // faithful floor-division grid (Kernel.cu:184)
+    const size_t pix = (size_t)ly * P.width + x;
+
+    uint32_t* st = P.state + pix * 12;
+    const uint4 s03 = *reinterpret_cast<const uint4*>(st);
+    const uint2 s45 = *reinterpret_cast<const uint2*>(st + 4);
+    Rng rng{s03.x, s03.y, s03.z, s03.w, s45.x, s45.y};
+
+    const f3 origin = mk(P.origin[0], P.origin[1], P.origin[2]);
+    const f3 up = mk(P.up[0], P.up[1], P.up[2]);
+    const f3 right = mk(P.right[0], P.right[1], P.right[2]);
+    const f3 fov_fwd = mk(P.fov_fwd[0], P.fov_fwd[1], P.fov_fwd[2]);
+    const f3 k10_fwd = mk(P.k10_fwd[0], P.k10_fwd[1], P.k10_fwd[2]);
+    const f3 bg0 = mk(P.bg0[0], P.bg0[1], P.bg0[2]);
+    const f3 bg1 = mk(P.bg1[0], P.bg1[1], P.bg1[2]);
+    const bool rtl = P.rius_rtl != 0;
+    const float xf = (float)(int)x - P.cx;       // (x - center.x())     (Kernel.cu:139)
+    const float yf = P.cy - (float)(int)g;       // (center.y() - y)     (Kernel.cu:140)
+
+    Counts cnt{0, 0, 0, 0};
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    uint32_t sample = 0, depth = 0;
+    bool need_camera = true;
+
+    if (P.spp > 0) {
+        while (true) {
+            if (need_camera) {  // camera ray (Kernel.cu:139-146)
+                const float u = (xf + uniform(rng)) / P.width_f;
+                const float v = (yf + uniform(rng)) / P.width_f;
+                const f3 dist = add(scale(u, right), scale(v, up));
+                const f3 start = add(add(scale(P.near_plane, dist), origin), fov_fwd);
+                const f3 second = add(add(scale(P.far_plane, dist), k10_fwd), origin);
+                ro = start;
+                rd = normalize(sub(second, start));
+                att = mk(1.0f, 1.0f, 1.0f);
+                depth = 0;
+                need_camera = false;
+                cnt.primary++;
+            }
+            f3 contrib;
+            bool done = true;
+            if (depth >= P.max_depth) {
+                contrib = mk(0.0f, 0.0f, 0.0f);  // exceeded recursion (Kernel.cu:79)
+            } else {
+                cnt.rays++;
+                const float a_dd = dot(rd, rd);
+                float t;
+                const int hit = trace<STACK, COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, lds_stack, cnt);
+                if (hit < 0) {  // sky (Kernel.cu:41-44)
+                    const f3 unit_direction = unit_vector(rd);
+                    const float tt = 0.5f * (unit_direction.y + 1.0f);
+                    const f3 c = add(scale(1.0f - tt, bg0), scale(tt, bg1));
+                    contrib = mulv(att, c);
+                } else {
+                    const float4 p0 = prims[2 * hit + 0];
+                    const float4 p1 = prims[2 * hit + 1];
+                    const uint32_t tag = __float_as_uint(p1.w);
+                    const uint32_t type = tag & 15u, mat = tag >> 4;
+                    const float4 m0 = P.mats[3 * mat + 0];
+                    const uint32_t mbits = __float_as_uint(m0.x);
+                    const uint32_t mtype = mbits & 15u, ttype = (mbits >> 4) & 15u;
+                    f3 p, normal;
+                    float hu = 0.0f, hv = 0.0f;
+                    if (type == RT_SPHERE) {
+                        p = add(ro, scale(t, rd));
+                        normal = divs(sub(p, xyz(p0)), p0.w);
+                        if (ttype == RT_IMAGE && mtype != RT_DIELECTRIC) {  // GetSphereUV (Hittable.cuh:119-125)
+                            const float theta = acosf(-normal.y);
+                            const float phi = atan2f(-normal.z, normal.x) + 3.141592654f;
+                            hu = phi / (2 * 3.141592654f);
+                            hv = theta / 3.141592654f;
+                        }
+                    } else {
+                        const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+                        const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+                        const float xx = oa + t * da;
+                        const float yy = ob + t * db;
+                        hu = (xx - p0.y) / (p0.z - p0.y);
+                        hv = (yy - p0.w) / (p1.x - p0.w);
+                        const f3 outward = type == RT_XYRECT ? mk(0.0f, 0.0f, 1.0f)
+                                           : type == RT_XZRECT ? mk(0.0f, 1.0f, 0.0f)
+                                                               : mk(1.0f, 0.0f, 0.0f);
+                        const bool front = dot(rd, outward) < 0;  // SetFaceNormal (Hittable.cuh:23-27)
+                        normal = front ? outward : neg(outward);
+                        p = add(ro, scale(t, rd));
+                    }
+                    if (mtype == RT_DIFFUSELIGHT) {  // DiffuseLight::Emitted (Material.cuh:164-176)
+                        const float4 m1 = P.mats[3 * mat + 1], m2 = P.mats[3 * mat + 2];
+                        const f3 e = scale(m0.z, texture_value(m0, m1, m2, ttype, hu, hv, p, P.imgs, P.texels));
+                        contrib = mulv(e, att);
+                    } else if (mtype == RT_DIELECTRIC) {  // Dielectric::Scatter (Material.cuh:106-136)
+                        const float ir = m0.y;
+                        const f3 reflected = reflect(rd, normal);
+                        f3 outward_normal;
+                        float ni_over_nt, cosine;
+                        if (dot(rd, normal) > 0.0f) {
+                            outward_normal = neg(normal);
+                            ni_over_nt = ir;
+                            cosine = dot(rd, normal) / length(rd);
+                            cosine = sqrtf(1.0f - ir * ir * (1 - cosine * cosine));
+                        } else {
+                            outward_normal = normal;
+                            ni_over_nt = 1.0f / ir;
+                            cosine = -dot(rd, normal) / length(rd);
+                        }
+                        // Refract (Math.cuh:292-304)
+                        const f3 uv = unit_vector(rd);
+                        const float dt = dot(uv, outward_normal);
+                        const float discriminant = 1.0f - ni_over_nt * ni_over_nt * (1 - dt * dt);
+                        f3 refracted = mk(0.0f, 0.0f, 0.0f);
+                        float reflect_prob = 1.0f;
+                        if (discriminant > 0) {
+                            refracted = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))),
+                                            scale(sqrtf(discriminant), outward_normal));
+                            float r0 = (1.0f - ir) / (1.0f + ir);  // Reflectance (Material.cuh:139-145)
+                            r0 = r0 * r0;
+                            const float xs = 1.0f - cosine;
+                            const float x2 = xs * xs;
+                            reflect_prob = r0 + (1.0f - r0) * ((x2 * x2) * xs);
+                        }
+                        ro = p;
+                        rd = uniform(rng) < reflect_prob ? reflected : refracted;
+                        done = false;
+                    } else {
+                        const f3 q = random_in_unit_sphere(rng, rtl);
+                        const float4 m1 = P.mats[3 * mat + 1];
+                        f3 attenuation;
+                        bool ok = true;
+                        if (mtype == RT_LAMBERTIAN) {  // Lambertian::Scatter (Material.cuh:43-62)
+                            const f3 target = add(add(p, normal), q);
+                            rd = sub(target, p);
+                        } else {  // Metal::Scatter (Material.cuh:75-94)
+                            const f3 reflected = reflect(unit_vector(rd), normal);
+                            rd = add(reflected, scale(m0.y, q));
+                            ok = dot(rd, normal) > 0;
+                        }
+                        if (ttype == RT_CONSTANT) {
+                            attenuation = xyz(m1);
+                        } else {
+                            const float4 m2 = P.mats[3 * mat + 2];
+                            attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, P.imgs, P.texels);
+                        }
+                        ro = p;
+                        if (ok) {
+                            att = mulv(attenuation, att);
+                            done = false;
+                        } else {
+                            contrib = mulv(mk(0.0f, 0.0f, 0.0f), att);  // emitted * cur_attenuation
+                        }
+                    }
+                    if (!done) depth++;
+                }
+            }
+            if (done) {
+                col = add(col, contrib);
+                if (++sample == P.spp) break;
+                need_camera = true;
+            }
+        }
+    }
+
+    if (!(P.flags & RT_FLAG_NO_STATE_WRITEBACK)) {
+        *reinterpret_cast<uint4*>(st) = make_uint4(rng.d, rng.v0, rng.v1, rng.v2);
+        *reinterpret_cast<uint2*>(st + 4) = make_uint2(rng.v3, rng.v4);
+    }
+    f3 c;
+    if (P.flags & RT_FLAG_ACCUMULATE) {
+        float4 a = P.accum[pix];
+        a.x = a.x + col.x;
+        a.y = a.y + col.y;
+        a.z = a.z + col.z;
+        a.w = a.w + (float)P.spp;
+        P.accum[pix] = a;
+        c = divs(mk(a.x, a.y, a.z), a.w);
+    } else {
+        c = divs(col, (float)P.spp);
+    }
+    if (P.radiance) P.radiance[pix] = make_float4(c.x, c.y, c.z, 1.0f);
+    if (P.pos) P.pos[pix] = rgb_to_int(255.0f * sqrtf(c.x), 255.0f * sqrtf(c.y), 255.0f * sqrtf(c.z));
+
+    if (P.counters) {
+        atomicAdd(&P.counters[0], (unsigned long long)cnt.rays);
+        if (COUNT_TESTS) {
+            atomicAdd(&P.counters[1], (unsigned long long)cnt.boxes);
+            atomicAdd(&P.counters[2], (unsigned long long)cnt.prims);
+        }
+        atomicAdd(&P.counters[3], (unsigned long long)cnt.primary);
+    }
+}
+
+// RenderInit (Kernel.cu:166-176): curand_init(seed_base + global_pixel_index, 0, 0).
+__device__ __forceinline__ void curand_init_state(unsigned long long seed, uint32_t* st) {
+    const uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+    const uint32_t s1 = ((uint32_t)(seed >> 32)) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    *reinterpret_cast<uint4*>(st) = make_uint4(6615241u + t1 + t0, 123456789u + t0, 362436069u ^ t0, 521288629u + t1);
+    *reinterpret_cast<uint4*>(st + 4) = make_uint4(88675123u ^ t1, 5783321u + t0, 0u, 0u);
+    *reinterpret_cast<uint4*>(st + 8) = make_uint4(0u, 0u, 0u, 0u);  // boxmuller_extra, pad, extra_double
+}
+
+__global__ __launch_bounds__(kBlock) void render_init_kernel(uint32_t* state, uint32_t width, uint32_t local_rows,
+                                                              uint32_t band_rows, uint32_t num_ranks, uint32_t rank,
+                                                              unsigned long long seed_base) {
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (size_t)width * local_rows) return;
+    const uint32_t ly = (uint32_t)(i / width), x = (uint32_t)(i - (size_t)ly * width);
+    const uint32_t band = ly / band_rows, within = ly - band * band_rows;
+    const uint32_t g = (band * num_ranks + rank) * band_rows + within;
+    const uint32_t pixel_index = g * width + x;  // unsigned, as Kernel.cu:174
+    curand_init_state(seed_base + pixel_index, state + i * 12);
+}
+
+// LaunchRenderInit's kernel honours the caller's grid/block exactly (Kernel.cu:166-176).
+__global__ void render_init_grid_kernel(uint32_t* state, uint32_t width, uint32_t height) {
+    const uint32_t i = threadIdx.x + blockIdx.x * blockDim.x;
+    const uint32_t j = threadIdx.y + blockIdx.y * blockDim.y;
+    if (i >= width || j >= height) return;
+    const uint32_t pixel_index = j * width + i;
+    curand_init_state(1984ull + pixel_index, state + (size_t)pixel_index * 12);
+}
+
+__global__ void rand_init_kernel(uint32_t* state) {  // RandInit (Kernel.cu:160-164)
+    if (threadIdx.x == 0 && blockIdx.x == 0) curand_init_state(1984ull, state);
+}
+
+}  // namespace dev
+
+// ---------------------------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+thread_local bool g_timing = false;
+thread_local float g_last_ms = -1.0f;
+thread_local int g_variant = -1;
+
+int hip_check(hipError_t e, const char* what, int code = RT_ERR_DEVICE) {
+    if (e == hipSuccess) return RT_OK;
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return code;
+}
+
+using KernelFn = void (*)(const dev::KParams);
+
+template <bool L, int S>
+KernelFn pick_count(bool count) {
+    return count ? dev::render_kernel<L, S, true> : dev::render_kernel<L, S, false>;
+}
+
+// variant = scene_lds * 3 + stack_kind
+KernelFn pick(int variant, bool count) {
+    switch (variant) {
+    case 0: return pick_count<false, dev::STACK_SCRATCH>(count);
+    case 1: return pick_count<false, dev::STACK_LDS>(count);
+    case 2: return pick_count<false, dev::STACK_HYBRID>(count);
+    case 3: return pick_count<true, dev::STACK_SCRATCH>(count);
+    case 4: return pick_count<true, dev::STACK_LDS>(count);
+    default: return pick_count<true, dev::STACK_HYBRID>(count);
+    }
+}
+
+constexpr size_t kLdsLimit = 160 * 1024;
+
+}  // namespace
+
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" {
+
+int rt_set_timing(int enabled) {
+    g_timing = enabled != 0;
+    return RT_OK;
+}
+
+float rt_last_kernel_ms(void) { return g_last_ms; }
+
+// Benchmark/tuning knob: -1 = automatic; 0..5 = (scene in LDS) * 3 + stack kind (0 scratch, 1 LDS,
+// 2 registers + scratch).  Returns the previous value.
+int rt_set_variant(int variant) {
+    int prev = g_variant;
+    g_variant = variant;
+    return prev;
+}
+
+int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) {
+    if (!scene || !a) { set_error("rt_render: NULL scene or args"); return RT_ERR_INVALID_ARGUMENT; }
+    if (!a->state) { set_error("rt_render: state is NULL"); return RT_ERR_INVALID_ARGUMENT; }
+    if (!a->pos && !a->radiance && !a->accum) { set_error("rt_render: no output buffer"); return RT_ERR_INVALID_ARGUMENT; }
+    if ((a->flags & RT_FLAG_ACCUMULATE) && !a->accum) { set_error("rt_render: ACCUMULATE without accum"); return RT_ERR_INVALID_ARGUMENT; }
+    if (a->width == 0 || a->height == 0) return RT_OK;
+    const rt_tiling& T = a->tiling;
+    if (T.band_rows == 0 || T.num_ranks == 0 || T.rank >= T.num_ranks) {
+        set_error("rt_render: invalid tiling");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    if (T.local_rows == 0) return RT_OK;
+    {
+        // the last local row must map into the image
+        uint32_t l = T.local_rows - 1, band = l / T.band_rows, within = l % T.band_rows;
+        uint64_t g = ((uint64_t)band * T.num_ranks + T.rank) * T.band_rows + within;
+        if (g >= a->height) { set_error("rt_render: tiling maps local rows outside the image"); return RT_ERR_INVALID_ARGUMENT; }
+    }
+    const DeviceScene& S = scene->dev;
+    if (S.depth > (uint32_t)dev::kStackMax) {
+        set_error("rt_render: BVH deeper than the traversal stack");
+        return RT_ERR_UNSUPPORTED;
+    }
+    dev::KParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.nodes = (const float4*)S.nodes;
+    P.prims = (const float4*)S.prims;
+    P.mats = (const float4*)S.mats;
+    P.imgs = (const int4*)S.imgs;
+    P.texels = (const uint8_t*)S.texels;
+    P.pos = a->pos;
+    P.radiance = (float4*)a->radiance;
+    P.accum = (float4*)a->accum;
+    P.state = (uint32_t*)a->state;
+    P.counters = (unsigned long long*)a->counters;
+    P.num_nodes = S.num_nodes;
+    P.num_prims = S.num_prims;
+    P.width = a->width;
+    P.height = a->height;
+    P.spp = a->samples_per_pixel;
+    P.max_depth = a->max_depth;
+    P.flags = a->flags;
+    P.band_rows = T.band_rows;
+    P.num_ranks = T.num_ranks;
+    P.rank = T.rank;
+    P.local_rows = T.local_rows;
+    P.tiles_x = (a->width + 15) / 16;
+    const bool faithful = (a->flags & RT_FLAG_FAITHFUL_GRID) != 0;
+    P.grid_w = faithful ? (a->width / 16) * 16 : a->width;
+    P.grid_h = faithful ? (a->height / 16) * 16 : a->height;
+    P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
+    // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
+    const rt_input_struct& in = a->inputs;
+    P.width_f = (float)a->width;
+    P.cx = (float)a->width / 2.0f;
+    P.cy = (float)a->height / 2.0f;
+    P.near_plane = in.near_plane;
+    P.far_plane = in.far_plane;
+    {
+        volatile float up[3] = {in.up[0], in.up[1], in.up[2]};
+        volatile float fw[3] = {in.orientation[0], in.orientation[1], in.orientation[2]};
+        // rightV = Normalize(Cross(upV, forwardV)) (Kernel.cu:133, Math.cuh:157-161, 225-229)
+        volatile float cx = up[1] * fw[2] - up[2] * fw[1];
+        volatile float t = up[0] * fw[2] - up[2] * fw[0];
+        volatile float cy = -t;
+        volatile float cz = up[0] * fw[1] - up[1] * fw[0];
+        volatile float d0 = cx * cx, d1 = cy * cy, d2 = cz * cz;
+        volatile float dd = d0 + d1;
+        dd = dd + d2;
+        volatile float s = std::sqrt((float)dd);
+        volatile float inv = 1.0f / s;
+        P.right[0] = inv * cx;
+        P.right[1] = inv * cy;
+        P.right[2] = inv * cz;
+        volatile float k10 = 1.0f / in.fov;
+        k10 = k10 * 10.0f;
+        for (int i = 0; i < 3; i++) {
+            P.origin[i] = in.origin[i];
+            P.up[i] = in.up[i];
+            P.fov_fwd[i] = in.fov * fw[i];
+            P.k10_fwd[i] = k10 * fw[i];
+            P.bg0[i] = in.background_start[i];
+            P.bg1[i] = in.background_end[i];
+        }
+    }
+
+    const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
+    const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
+    int variant = g_variant;
+    if (variant < 0) variant = scene_lds <= 48 * 1024 ? 3 : 0;  // auto: scene in LDS when it fits
+    const bool v_lds = variant >= 3;
+    const int v_stack = variant % 3;
+    if (v_stack == dev::STACK_LDS && S.depth > (uint32_t)dev::kLdsStackDepth + 1) {
+        set_error("rt_render: BVH too deep for the LDS stack variant");
+        return RT_ERR_UNSUPPORTED;
+    }
+    size_t lds_bytes = (v_lds ? scene_lds : 0) +
+                       (v_stack == dev::STACK_LDS ? (size_t)dev::kLdsStackDepth * dev::kBlock * 4 : 0);
+    if (lds_bytes > kLdsLimit) {
+        set_error("rt_render: scene does not fit in LDS for this variant");
+        return RT_ERR_UNSUPPORTED;
+    }
+    KernelFn fn = pick(variant, count_tests);
+    const uint32_t tiles = P.tiles_x * ((T.local_rows + 15) / 16);
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing) {
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipEventRecord(e0, s);
+    }
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(fn, dim3(tiles), dim3(dev::kBlock), lds_bytes, s, P);
+    int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
+    if (g_timing) {
+        (void)hipEventRecord(e1, s);
+        if (rc == RT_OK && hipEventSynchronize(e1) == hipSuccess) {
+            float ms = -1.0f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            g_last_ms = ms;
+        } else {
+            g_last_ms = -1.0f;
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    return rc;
+}
+
+int rt_render_init(rt_curand_state* d_state, uint32_t width, uint32_t height, const rt_tiling* tiling,
+                   uint64_t seed_base, rt_stream stream) {
+    if (!d_state || !tiling) { set_error("rt_render_init: NULL argument"); return RT_ERR_INVALID_ARGUMENT; }
+    if (tiling->band_rows == 0 || tiling->num_ranks == 0 || tiling->rank >= tiling->num_ranks) {
+        set_error("rt_render_init: invalid tiling");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    (void)height;
+    const size_t n = (size_t)width * tiling->local_rows;
+    if (n == 0) return RT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(dev::render_init_kernel, dim3((unsigned)((n + dev::kBlock - 1) / dev::kBlock)), dim3(dev::kBlock), 0,
+                       (hipStream_t)stream, (uint32_t*)d_state, width, tiling->local_rows, tiling->band_rows,
+                       tiling->num_ranks, tiling->rank, (unsigned long long)seed_base);
+    return hip_check(hipGetLastError(), "rt_render_init: kernel launch", RT_ERR_LAUNCH);
+}
+
+// ----- reference-named drop-in launchers (synchronous, void) ----------------------------------------
+
+void LaunchRenderInit(rt_dim3 grid, rt_dim3 block, unsigned int window_width, unsigned int window_height,
+                      rt_curand_state* d_rand_state) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(dev::render_init_grid_kernel, dim3(grid.x, grid.y, grid.z), dim3(block.x, block.y, block.z), 0, 0,
+                       (uint32_t*)d_rand_state, window_width, window_height);
+    if (hip_check(hipGetLastError(), "LaunchRenderInit: kernel launch", RT_ERR_LAUNCH) == RT_OK)
+        hip_check(hipDeviceSynchronize(), "LaunchRenderInit: hipDeviceSynchronize");
+}
+
+void LaunchRandInit(rt_curand_state* d_rand_state2) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(dev::rand_init_kernel, dim3(1), dim3(1), 0, 0, (uint32_t*)d_rand_state2);
+    if (hip_check(hipGetLastError(), "LaunchRandInit: kernel launch", RT_ERR_LAUNCH) == RT_OK)
+        hip_check(hipDeviceSynchronize(), "LaunchRandInit: hipDeviceSynchronize");
+}
+
+void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int image_height,
+                  const unsigned int samples_per_pixel, const unsigned int max_depth, const void* world,
+                  rt_curand_state* d_rand_state, rt_input_struct inputs) {
+    // The viewer mutates the graph in place between frames: re-flatten every call,
+    // re-upload only when the flattened scene changed.
+    static std::mutex mu;
+    static std::vector<uint8_t> last_key;
+    static rt_scene* cached = nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    FlatDesc f;
+    std::string err;
+    if (flatten_reference_graph(world, &f, &err) != RT_OK) {
+        set_error("LaunchKernel: " + err);
+        return;
+    }
+    std::vector<uint8_t> key;
+    auto append = [&](const void* p, size_t n) { key.insert(key.end(), (const uint8_t*)p, (const uint8_t*)p + n); };
+    append(f.hittables.data(), f.hittables.size() * sizeof(rt_hittable_desc));
+    append(f.materials.data(), f.materials.size() * sizeof(rt_material_desc));
+    for (const rt_image_desc& im : f.images) {
+        append(&im, sizeof(im));
+        if (im.data) append(im.data, (size_t)im.width * im.height * 3);
+    }
+    if (!cached || key != last_key) {
+        rt_scene_destroy(cached);
+        cached = nullptr;
+        rt_scene_desc d = f.desc();
+        if (rt_scene_create(&d, &cached) != RT_OK) return;
+        last_key.swap(key);
+    }
+    rt_render_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.pos = pos;
+    a.state = d_rand_state;
+    a.width = image_width;
+    a.height = image_height;
+    a.samples_per_pixel = samples_per_pixel;
+    a.max_depth = max_depth;
+    a.flags = RT_FLAG_FAITHFUL_GRID;
+    a.tiling.band_rows = image_height ? image_height : 1;
+    a.tiling.num_ranks = 1;
+    a.tiling.rank = 0;
+    a.tiling.local_rows = image_height;
+    a.inputs = inputs;
+    if (rt_render(cached, &a, nullptr) != RT_OK) return;
+    hip_check(hipDeviceSynchronize(), "LaunchKernel: hipDeviceSynchronize");  // Kernel.cu:190
+}
+
+}  // extern "C"

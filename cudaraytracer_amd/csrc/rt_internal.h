@@ -1,0 +1,86 @@
+// rt_internal.h — internal (non-ABI) definitions shared by the host scene builder and the gfx950 kernels.
+//
+// Device data layout (all tables are read-only during a launch and small: an RTIOW scene of 488 spheres
+// is ~40 KB, so a workgroup can stage the node + primitive tables in LDS):
+//
+//   nodes   : BVH2 with the two child boxes stored in the parent (4 × float4 = 64 B per node):
+//               n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+//               n1 = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//               n2 = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+//               n3 = (int c0, int c1, 0, 0)    child >= 0: internal node; child < 0: leaf ~(first<<4 | count)
+//   prims   : 2 × float4 = 32 B per primitive, in BVH leaf order:
+//               sphere: p0 = (cx, cy, cz, r),         p1 = (r·r, 0, 0, bits(type | mat << 4))
+//               rect  : p0 = (k, a0, a1, b0),         p1 = (b1, 0, 0, bits(type | mat << 4))
+//                       k = plane coordinate, [a0,a1]×[b0,b1] the in-plane extent, exactly the floats
+//                       XYRect/XZRect/YZRect::Hit compute (Hittable.cuh:142-147, 198-203, 254-259)
+//   mats    : 3 × float4 = 48 B per material:
+//               m0 = (bits(type | textype << 4), fuzz|ir, float(light_intensity), bits(image))
+//               m1 = (color.rgb, 0)   m2 = (color2.rgb, 0)
+//   images  : RGB8 texels of every image back to back; imgs[i] = (offset, width, height, 0) as int4
+//
+// Box padding: child boxes are the reference's primitive boxes (Hittable.cuh:112-116, 171-181, ...)
+// grown outward by a relative epsilon, so the fused-multiply-add slab test of the kernel can never
+// reject a primitive the exact test would accept.  Boxes only cull: the closest hit is decided by the
+// primitive tests, which follow the reference arithmetic exactly.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+
+namespace rt {
+
+constexpr int kLeafMax = 4;         // max primitives per leaf
+constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) traversal stack
+
+struct HostScene {
+    std::vector<float> nodes;   // 16 floats per node
+    std::vector<float> prims;   // 8 floats per primitive
+    std::vector<float> mats;    // 12 floats per material
+    std::vector<int32_t> imgs;  // 4 ints per image
+    std::vector<uint8_t> texels;
+    uint32_t num_nodes = 0;
+    uint32_t num_prims = 0;
+    uint32_t num_mats = 0;
+    uint32_t depth = 0;          // max root-to-leaf node count
+    bool has_image_textures = false;
+    std::vector<int32_t> prim_source;  // desc index of each primitive (BVH order)
+};
+
+// Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.
+int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err);
+
+// Material table packing only (used by rt_scene_update_materials).
+int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images, std::vector<float>* out,
+                   std::string* err);
+
+// Flatten the reference's pointer graph (rt_reference_graph.h) into a flat description.
+struct FlatDesc {
+    std::vector<rt_hittable_desc> hittables;
+    std::vector<rt_material_desc> materials;
+    std::vector<rt_image_desc> images;
+    rt_scene_desc desc() const {
+        rt_scene_desc d;
+        d.hittables = hittables.data();
+        d.num_hittables = (uint32_t)hittables.size();
+        d.materials = materials.data();
+        d.num_materials = (uint32_t)materials.size();
+        d.images = images.data();
+        d.num_images = (uint32_t)images.size();
+        return d;
+    }
+};
+int flatten_reference_graph(const void* world, FlatDesc* out, std::string* err);
+
+void set_error(const std::string& msg);
+
+inline float bits_to_float(uint32_t u) {
+    float f;
+    static_assert(sizeof(f) == sizeof(u), "");
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+
+}  // namespace rt

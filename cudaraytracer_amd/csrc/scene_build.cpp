@@ -1,0 +1,299 @@
+// scene_build.cpp — host side of the scene boundary: validation, flat-table packing and the BVH build.
+//
+// Replaces the reference's host-side scene construction: the managed-memory pointer graph of
+// CudaLayer::GenerateWorld (CudaLayer.cpp:103-256) and the recursive BVHNode constructor
+// (Hittable.cuh:303-385).  The reference splits by hittable type, then in list order (no spatial
+// criterion), which costs ~50 box tests per ray on the RTIOW scene.  Here a full-sweep
+// SAH build over padded reference boxes produces a BVH with the same closest-hit semantics: the
+// primitive tests alone decide the hit, boxes only cull (see rt_internal.h).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+#include "rt_internal.h"
+
+namespace rt {
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+    void empty() {
+        for (int i = 0; i < 3; i++) { lo[i] = INFINITY; hi[i] = -INFINITY; }
+    }
+    void grow(const Box& b) {
+        for (int i = 0; i < 3; i++) { lo[i] = std::min(lo[i], b.lo[i]); hi[i] = std::max(hi[i], b.hi[i]); }
+    }
+    float area() const {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0f;
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+// Rect plane/extent exactly as XYRect/XZRect/YZRect::Hit compute them (Hittable.cuh:142-147, 198-203,
+// 254-259): a0 = c.a - (w / 2) etc.  Evaluated in binary32 so the device sees identical floats.
+struct RectGeom { float k, a0, a1, b0, b1; int ia, ib, ik; };
+RectGeom rect_geom(const rt_hittable_desc& h) {
+    RectGeom g;
+    const float* c = h.center;
+    volatile float w2 = h.width / 2, h2 = h.height / 2;  // keep binary32 rounding of each step
+    if (h.type == RT_XYRECT) {
+        g.a0 = c[0] - w2; g.a1 = c[0] + w2; g.b0 = c[1] - h2; g.b1 = c[1] + h2; g.k = c[2];
+        g.ia = 0; g.ib = 1; g.ik = 2;
+    } else if (h.type == RT_XZRECT) {
+        g.a0 = c[0] - w2; g.a1 = c[0] + w2; g.b0 = c[2] - h2; g.b1 = c[2] + h2; g.k = c[1];
+        g.ia = 0; g.ib = 2; g.ik = 1;
+    } else {  // YZ: y from height, z from width
+        g.a0 = c[1] - h2; g.a1 = c[1] + h2; g.b0 = c[2] - w2; g.b1 = c[2] + w2; g.k = c[0];
+        g.ia = 1; g.ib = 2; g.ik = 0;
+    }
+    return g;
+}
+
+// Reference primitive box (Hittable.cuh:112-116, 171-181, 227-237, 283-293), grown outward.
+Box prim_box(const rt_hittable_desc& h) {
+    Box b;
+    if (h.type == RT_SPHERE) {
+        for (int i = 0; i < 3; i++) { b.lo[i] = h.center[i] - h.radius; b.hi[i] = h.center[i] + h.radius; }
+    } else {
+        RectGeom g = rect_geom(h);
+        b.lo[g.ia] = g.a0; b.hi[g.ia] = g.a1;
+        b.lo[g.ib] = g.b0; b.hi[g.ib] = g.b1;
+        b.lo[g.ik] = g.k - 0.0001f; b.hi[g.ik] = g.k + 0.0001f;
+    }
+    for (int i = 0; i < 3; i++) {
+        float m = std::max(std::fabs(b.lo[i]), std::fabs(b.hi[i]));
+        float pad = 1e-5f * m + 1e-6f;
+        b.lo[i] -= pad;
+        b.hi[i] += pad;
+    }
+    return b;
+}
+
+struct BuildPrim {
+    Box box;
+    float centroid[3];
+    int src;  // index into desc.hittables
+};
+
+struct Builder {
+    std::vector<BuildPrim> prims;
+    std::vector<int> order;  // final primitive order
+    struct Node {
+        Box box[2];
+        int child[2];
+    };
+    std::vector<Node> nodes;
+    uint32_t max_depth = 0;
+
+    Box range_box(int b, int e) const {
+        Box r;
+        r.empty();
+        for (int i = b; i < e; i++) r.grow(prims[order[i]].box);
+        return r;
+    }
+
+    int make_leaf(int b, int e) const { return ~((b << 4) | (e - b)); }
+
+    // Returns the child reference for [b, e).
+    int build(int b, int e, uint32_t depth) {
+        int n = e - b;
+        if (depth > max_depth) max_depth = depth;
+        const bool must_split = depth == 1;  // the root is always an internal node (see build_root)
+        if (n <= 1 && !must_split) return make_leaf(b, e);
+        // Full-sweep SAH over the three centroid axes.
+        float best_cost = INFINITY;
+        int best_axis = -1, best_split = -1;
+        std::vector<int> tmp(order.begin() + b, order.begin() + e);
+        std::vector<float> right_area(n);
+        for (int axis = 0; axis < 3; axis++) {
+            std::stable_sort(tmp.begin(), tmp.end(), [&](int x, int y) {
+                return prims[x].centroid[axis] < prims[y].centroid[axis];
+            });
+            Box acc;
+            acc.empty();
+            for (int i = n - 1; i > 0; i--) {
+                acc.grow(prims[tmp[i]].box);
+                right_area[i] = acc.area();
+            }
+            acc.empty();
+            for (int i = 1; i < n; i++) {
+                acc.grow(prims[tmp[i - 1]].box);
+                float cost = acc.area() * (float)i + right_area[i] * (float)(n - i);
+                if (cost < best_cost) { best_cost = cost; best_axis = axis; best_split = i; }
+            }
+        }
+        Box all = range_box(b, e);
+        float leaf_cost = all.area() * (float)n;
+        const float kTraversal = 1.2f;  // cost of one node visit relative to one primitive test
+        if (!must_split && n <= kLeafMax && best_cost + kTraversal * all.area() >= leaf_cost) return make_leaf(b, e);
+        std::stable_sort(order.begin() + b, order.begin() + e, [&](int x, int y) {
+            return prims[x].centroid[best_axis] < prims[y].centroid[best_axis];
+        });
+        int mid = b + best_split;
+        int id = (int)nodes.size();
+        nodes.push_back(Node());
+        int l = build(b, mid, depth + 1);
+        int r = build(mid, e, depth + 1);
+        nodes[id].child[0] = l;
+        nodes[id].child[1] = r;
+        nodes[id].box[0] = range_box(b, mid);
+        nodes[id].box[1] = range_box(mid, e);
+        return id;
+    }
+
+    void build_root() {
+        int n = (int)prims.size();
+        order.resize(n);
+        std::iota(order.begin(), order.end(), 0);
+        if (n == 0) return;
+        if (n == 1) {
+            // Root with both children referencing the single leaf (a second test of the same primitive
+            // cannot change the closest hit: Sphere::Hit is strict in t_max, rects re-accept the same t).
+            nodes.push_back(Node());
+            nodes[0].child[0] = nodes[0].child[1] = make_leaf(0, 1);
+            nodes[0].box[0] = nodes[0].box[1] = prims[0].box;
+            max_depth = 2;
+            return;
+        }
+        max_depth = 1;
+        int r = build(0, n, 1);
+        (void)r;  // n >= 2 always yields an internal root at index 0
+    }
+};
+
+int check_texture(const rt_texture_desc& t, uint32_t num_images, std::string* err) {
+    if (t.type < RT_CONSTANT || t.type > RT_IMAGE) {
+        *err = "texture type " + std::to_string(t.type) + " is not CONSTANT/CHECKER/IMAGE";
+        return RT_ERR_INVALID_SCENE;
+    }
+    if (t.type == RT_IMAGE && t.image >= (int32_t)num_images) {
+        *err = "image texture index " + std::to_string(t.image) + " out of range";
+        return RT_ERR_INVALID_SCENE;
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images, std::vector<float>* out,
+                   std::string* err) {
+    out->assign((size_t)n * 12, 0.0f);
+    for (uint32_t i = 0; i < n; i++) {
+        const rt_material_desc& m = mats[i];
+        if (m.type < RT_LAMBERTIAN || m.type > RT_DIFFUSELIGHT) {
+            *err = "material " + std::to_string(i) + ": type " + std::to_string(m.type) + " invalid";
+            return RT_ERR_INVALID_SCENE;
+        }
+        if (m.type != RT_DIELECTRIC) {
+            int rc = check_texture(m.albedo, num_images, err);
+            if (rc) { *err = "material " + std::to_string(i) + ": " + *err; return rc; }
+        }
+        float* o = out->data() + (size_t)i * 12;
+        uint32_t tex_type = m.type == RT_DIELECTRIC ? 0u : (uint32_t)m.albedo.type;
+        o[0] = bits_to_float((uint32_t)m.type | (tex_type << 4));
+        o[1] = m.type == RT_METAL ? m.fuzz : (m.type == RT_DIELECTRIC ? m.ir : 0.0f);
+        o[2] = (float)m.light_intensity;  // `light_intensity * value`: int → float (Material.cuh:168)
+        int32_t img = m.albedo.type == RT_IMAGE ? m.albedo.image : -1;
+        o[3] = bits_to_float((uint32_t)img);
+        for (int c = 0; c < 3; c++) {
+            o[4 + c] = m.albedo.color[c];
+            o[8 + c] = m.albedo.color2[c];
+        }
+    }
+    return RT_OK;
+}
+
+int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err) {
+    if (!desc) { *err = "scene description is NULL"; return RT_ERR_INVALID_ARGUMENT; }
+    if ((desc->num_hittables && !desc->hittables) || (desc->num_materials && !desc->materials) ||
+        (desc->num_images && !desc->images)) {
+        *err = "scene description has a NULL array with a non-zero count";
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    *out = HostScene();
+    int rc = pack_materials(desc->materials, desc->num_materials, desc->num_images, &out->mats, err);
+    if (rc) return rc;
+    out->num_mats = desc->num_materials;
+    for (uint32_t i = 0; i < desc->num_materials; i++)
+        if (desc->materials[i].type != RT_DIELECTRIC && desc->materials[i].albedo.type == RT_IMAGE)
+            out->has_image_textures = true;
+
+    // images
+    size_t off = 0;
+    for (uint32_t i = 0; i < desc->num_images; i++) {
+        const rt_image_desc& im = desc->images[i];
+        if (im.width < 0 || im.height < 0 || (im.data == nullptr && im.width * im.height != 0)) {
+            // data == NULL is allowed and means "no data" (Texture.cuh:83-84) when w·h == 0
+        }
+        size_t bytes = im.data ? (size_t)im.width * (size_t)im.height * 3 : 0;
+        out->imgs.push_back(im.data ? (int32_t)off : -1);
+        out->imgs.push_back(im.width);
+        out->imgs.push_back(im.height);
+        out->imgs.push_back(0);
+        if (bytes) {
+            out->texels.insert(out->texels.end(), im.data, im.data + bytes);
+            off += bytes;
+            off = (off + 15) & ~(size_t)15;
+            out->texels.resize(off, 0);
+        }
+    }
+
+    Builder B;
+    for (uint32_t i = 0; i < desc->num_hittables; i++) {
+        const rt_hittable_desc& h = desc->hittables[i];
+        if (!h.is_active) continue;  // thrust::remove_if of inactive objects (Hittable.cuh:311-312)
+        if (h.type < RT_SPHERE || h.type > RT_YZRECT) {
+            *err = "hittable " + std::to_string(i) + ": type " + std::to_string(h.type) + " invalid";
+            return RT_ERR_INVALID_SCENE;
+        }
+        if (h.material < 0 || (uint32_t)h.material >= desc->num_materials) {
+            *err = "hittable " + std::to_string(i) + ": material index " + std::to_string(h.material) +
+                   " out of range";
+            return RT_ERR_INVALID_SCENE;
+        }
+        BuildPrim p;
+        p.box = prim_box(h);
+        for (int a = 0; a < 3; a++) p.centroid[a] = 0.5f * (p.box.lo[a] + p.box.hi[a]);
+        p.src = (int)i;
+        B.prims.push_back(p);
+    }
+    B.build_root();
+    out->num_prims = (uint32_t)B.prims.size();
+    out->num_nodes = (uint32_t)B.nodes.size();
+    out->depth = B.max_depth;
+
+    out->nodes.resize((size_t)out->num_nodes * 16);
+    for (uint32_t i = 0; i < out->num_nodes; i++) {
+        const Builder::Node& n = B.nodes[i];
+        float* o = out->nodes.data() + (size_t)i * 16;
+        o[0] = n.box[0].lo[0]; o[1] = n.box[0].hi[0]; o[2] = n.box[0].lo[1]; o[3] = n.box[0].hi[1];
+        o[4] = n.box[1].lo[0]; o[5] = n.box[1].hi[0]; o[6] = n.box[1].lo[1]; o[7] = n.box[1].hi[1];
+        o[8] = n.box[0].lo[2]; o[9] = n.box[0].hi[2]; o[10] = n.box[1].lo[2]; o[11] = n.box[1].hi[2];
+        o[12] = bits_to_float((uint32_t)n.child[0]);
+        o[13] = bits_to_float((uint32_t)n.child[1]);
+        o[14] = 0.0f;
+        o[15] = 0.0f;
+    }
+    out->prims.resize((size_t)out->num_prims * 8);
+    out->prim_source.resize(out->num_prims);
+    for (uint32_t i = 0; i < out->num_prims; i++) {
+        const rt_hittable_desc& h = desc->hittables[B.prims[B.order[i]].src];
+        out->prim_source[i] = B.prims[B.order[i]].src;
+        float* o = out->prims.data() + (size_t)i * 8;
+        uint32_t tag = (uint32_t)h.type | ((uint32_t)h.material << 4);
+        if (h.type == RT_SPHERE) {
+            o[0] = h.center[0]; o[1] = h.center[1]; o[2] = h.center[2]; o[3] = h.radius;
+            o[4] = h.radius * h.radius; o[5] = 0.0f; o[6] = 0.0f;
+        } else {
+            RectGeom g = rect_geom(h);
+            o[0] = g.k; o[1] = g.a0; o[2] = g.a1; o[3] = g.b0;
+            o[4] = g.b1; o[5] = 0.0f; o[6] = 0.0f;
+        }
+        o[7] = bits_to_float(tag);
+    }
+    return RT_OK;
+}
+
+}  // namespace rt

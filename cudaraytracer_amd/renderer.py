@@ -1,0 +1,133 @@
+"""Host-side mirror of the reference's render caller (CudaLayer, Cuda/CudaLayer.cpp) over the C ABI.
+
+`Renderer` owns the device framebuffer and RNG-state buffers (InitCudaBuffers, CudaLayer.cpp:68-74), seeds
+the RNG (RunCudaInit → RenderInit, CudaLayer.cpp:93-101), holds the device scene (GenerateWorld,
+CudaLayer.cpp:103-256) and renders frames (RunCudaUpdate → LaunchKernel, CudaLayer.cpp:372-375).  Device
+memory is allocated through torch (plumbing only); every compute step is a librt_hip.so call.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import abi
+from ._lib import RTError, check, lib
+from .scenes import Scene
+
+
+class DeviceScene:
+    """rt_scene handle (device-resident BVH + primitive + material tables)."""
+
+    def __init__(self, scene: Scene | None = None, reference_graph: int | None = None):
+        L = lib()
+        self.handle = C.c_void_p()
+        self.scene = scene
+        if reference_graph is not None:
+            check(L.rt_scene_from_reference_graph(C.c_void_p(reference_graph), C.byref(self.handle)),
+                  "rt_scene_from_reference_graph")
+        else:
+            self._desc = scene.desc()
+            check(L.rt_scene_create(C.byref(self._desc), C.byref(self.handle)), "rt_scene_create")
+
+    def info(self) -> abi.SceneInfo:
+        out = abi.SceneInfo()
+        check(lib().rt_scene_get_info(self.handle, C.byref(out)), "rt_scene_get_info")
+        return out
+
+    def update_materials(self, materials) -> None:
+        check(lib().rt_scene_update_materials(self.handle, C.cast(materials, C.POINTER(abi.MaterialDesc)),
+                                              len(materials)), "rt_scene_update_materials")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().rt_scene_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def band_rows_of(height: int, band_rows: int, num_ranks: int, rank: int) -> list[int]:
+    """Global rows owned by `rank` under block-cyclic row bands (rt_tiling, include/rt_hip.h)."""
+    rows = []
+    b = rank
+    while b * band_rows < height:
+        rows.extend(range(b * band_rows, min(height, (b + 1) * band_rows)))
+        b += num_ranks
+    return rows
+
+
+class Renderer:
+    """One rank's share of a W×H image (all of it when num_ranks = 1)."""
+
+    def __init__(self, width: int, height: int, device: int | str = 0, band_rows: int | None = None,
+                 num_ranks: int = 1, rank: int = 0):
+        if not torch.cuda.is_available():
+            raise RTError("no HIP device visible: librt_hip.so renders on MI355X only")
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        torch.cuda.set_device(self.device)
+        check(lib().rt_set_device(self.device.index or 0), "rt_set_device")
+        self.width, self.height = width, height
+        self.band_rows = band_rows or height
+        self.num_ranks, self.rank = num_ranks, rank
+        self.rows = band_rows_of(height, self.band_rows, num_ranks, rank)
+        self.local_rows = len(self.rows)
+        n = width * self.local_rows
+        # InitCudaBuffers (CudaLayer.cpp:68-74): RGBA8 framebuffer + one 48-byte curandState per pixel
+        self.pos = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self.state = torch.zeros(n * abi.STATE_WORDS, dtype=torch.int32, device=self.device)
+        self.counters = torch.zeros(4, dtype=torch.int64, device=self.device)
+        self.radiance = None
+        self.accum = None
+
+    def tiling(self) -> abi.Tiling:
+        return abi.Tiling(self.band_rows, self.num_ranks, self.rank, self.local_rows)
+
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def render_init(self, seed_base: int = 1984) -> None:
+        """RenderInit: curand_init(seed_base + global pixel index, 0, 0) (Kernel.cu:166-176)."""
+        t = self.tiling()
+        check(lib().rt_render_init(C.c_void_p(self.state.data_ptr()), self.width, self.height, C.byref(t),
+                                   seed_base, C.c_void_p(self.stream())), "rt_render_init")
+
+    def render(self, scene: DeviceScene, spp: int, max_depth: int, inputs: abi.InputStruct, flags: int = 0,
+               radiance: bool = False, count: bool = True) -> torch.Tensor:
+        """One frame (Kernel.cu:102-158), asynchronous on torch's current stream; returns `pos`."""
+        if radiance and self.radiance is None:
+            self.radiance = torch.zeros(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
+        if flags & abi.RT_FLAG_ACCUMULATE and self.accum is None:
+            self.accum = torch.zeros(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
+        a = abi.RenderArgs()
+        a.pos = self.pos.data_ptr()
+        a.radiance = self.radiance.data_ptr() if radiance else None
+        a.accum = self.accum.data_ptr() if self.accum is not None and flags & abi.RT_FLAG_ACCUMULATE else None
+        a.state = self.state.data_ptr()
+        a.counters = self.counters.data_ptr() if count else None
+        a.width, a.height = self.width, self.height
+        a.samples_per_pixel, a.max_depth = spp, max_depth
+        a.flags = flags
+        a.tiling = self.tiling()
+        a.inputs = inputs
+        check(lib().rt_render(scene.handle, C.byref(a), C.c_void_p(self.stream())), "rt_render")
+        return self.pos
+
+    def reset_accumulation(self) -> None:
+        if self.accum is not None:
+            self.accum.zero_()
+
+    def image(self) -> np.ndarray:
+        """Local framebuffer as (local_rows, W) uint32 RGBA8 (row 0 = bottom of the image)."""
+        return self.pos.cpu().numpy().view(np.uint32).reshape(self.local_rows, self.width)
+
+    def states(self) -> np.ndarray:
+        return self.state.cpu().numpy().view(np.uint32).reshape(-1, abi.STATE_WORDS)
+
+    def radiance_image(self) -> np.ndarray:
+        return self.radiance.cpu().numpy().reshape(self.local_rows, self.width, 4)

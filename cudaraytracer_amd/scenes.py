@@ -1,0 +1,166 @@
+"""Scene descriptions and the BASELINE.json configurations (host side, no GPU needed).
+
+`Scene` holds the flat description (rt_scene_desc) the C ABI takes: hittables in list order, one material
+per hittable (as CudaLayer::GenerateWorld allocates them, CudaLayer.cpp:103-256) and optional RGB8 images.
+The built-in generators live in librt_hip.so (csrc/builtin_scenes.cpp); the camera → InputStruct fill
+follows CudaLayer.cpp:43-65.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from ._lib import check, lib
+
+SCENE_DEFAULT_WORLD = 0
+SCENE_THREE_SPHERES = 1
+SCENE_RTIOW = 2
+SCENE_CORNELL = 3
+SCENE_TEXTURED = 4
+
+DEFAULT_BG_START = (1.0, 1.0, 1.0)  # CudaLayer.h:143
+DEFAULT_BG_END = (0.5, 0.7, 1.0)  # CudaLayer.h:144
+
+
+@dataclass
+class Scene:
+    hittables: C.Array
+    materials: C.Array
+    images: list = field(default_factory=list)  # numpy uint8 (H, W, 3) arrays, kept alive here
+    _image_descs: C.Array | None = None
+
+    @property
+    def num_hittables(self) -> int:
+        return len(self.hittables)
+
+    def desc(self) -> abi.SceneDesc:
+        imgs = (abi.ImageDesc * max(1, len(self.images)))()
+        for i, im in enumerate(self.images):
+            im = np.ascontiguousarray(im, dtype=np.uint8)
+            self.images[i] = im
+            imgs[i].data = im.ctypes.data
+            imgs[i].height, imgs[i].width = int(im.shape[0]), int(im.shape[1])
+        self._image_descs = imgs
+        return abi.SceneDesc(
+            C.cast(self.hittables, C.POINTER(abi.HittableDesc)),
+            len(self.hittables),
+            C.cast(self.materials, C.POINTER(abi.MaterialDesc)),
+            len(self.materials),
+            C.cast(imgs, C.POINTER(abi.ImageDesc)),
+            len(self.images),
+        )
+
+    def hittables_bytes(self) -> bytes:
+        return bytes(memoryview(self.hittables).cast("B"))
+
+    def materials_bytes(self) -> bytes:
+        return bytes(memoryview(self.materials).cast("B"))
+
+    @classmethod
+    def from_bytes(cls, hittables: bytes, materials: bytes, images=None) -> "Scene":
+        nh = len(hittables) // C.sizeof(abi.HittableDesc)
+        nm = len(materials) // C.sizeof(abi.MaterialDesc)
+        h = (abi.HittableDesc * nh).from_buffer_copy(hittables)
+        m = (abi.MaterialDesc * nm).from_buffer_copy(materials)
+        return cls(h, m, list(images or []))
+
+
+def procedural_texture(width: int = 512, height: int = 256) -> np.ndarray:
+    """Deterministic RGB8 'planet' texture standing in for assets/textures/8k_*.jpg (no JPEG decoder here)."""
+    v, u = np.meshgrid(np.linspace(0.0, 1.0, height, dtype=np.float64),
+                       np.linspace(0.0, 1.0, width, dtype=np.float64), indexing="ij")
+    lat = (v - 0.5) * np.pi
+    lon = u * 2.0 * np.pi
+    land = (np.sin(3.0 * lon) * np.cos(2.0 * lat) + 0.5 * np.sin(7.0 * lon + 1.3) * np.sin(5.0 * lat)) > 0.15
+    ice = np.abs(lat) > 1.25
+    r = np.where(ice, 235, np.where(land, 70 + 60 * np.cos(lat), 20))
+    g = np.where(ice, 240, np.where(land, 120 + 40 * np.sin(lon), 60))
+    b = np.where(ice, 250, np.where(land, 40, 150 + 60 * np.cos(lat)))
+    img = np.stack([r, g, b], axis=-1)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def builtin(which: int, seed: int = 1) -> Scene:
+    """Built-in scene `which` (see rt_builtin_scene in include/rt_hip.h)."""
+    L = lib()
+    nh, nm = C.c_uint32(0), C.c_uint32(0)
+    check(L.rt_builtin_scene(which, seed, None, C.byref(nh), None, C.byref(nm)), "rt_builtin_scene(size)")
+    h = (abi.HittableDesc * nh.value)()
+    m = (abi.MaterialDesc * nm.value)()
+    check(L.rt_builtin_scene(which, seed, h, C.byref(nh), m, C.byref(nm)), "rt_builtin_scene")
+    images = [procedural_texture()] if which == SCENE_TEXTURED else []
+    return Scene(h, m, images)
+
+
+def camera_inputs(position, orientation, fov_degrees, near=0.1, far=10.0, world_up=(0.0, 1.0, 0.0),
+                  bg_start=DEFAULT_BG_START, bg_end=DEFAULT_BG_END) -> abi.InputStruct:
+    """InputStruct from a Camera (Renderer/Camera.h:39-45) exactly as CudaLayer.cpp:43-65 fills it."""
+    F3 = C.c_float * 3
+    out = abi.InputStruct()
+    lib().rt_camera_inputs(F3(*position), F3(*orientation), F3(*world_up), fov_degrees, near, far,
+                           F3(*bg_start), F3(*bg_end), C.byref(out))
+    return out
+
+
+def normalized(v) -> tuple:
+    a = np.asarray(v, dtype=np.float32)
+    inv = np.float32(1.0) / np.sqrt(np.float32(a @ a), dtype=np.float32)
+    return tuple(float(x) for x in (a * inv).astype(np.float32))
+
+
+@dataclass
+class Config:
+    name: str
+    scene: int
+    width: int
+    height: int
+    spp: int
+    depth: int
+    position: tuple
+    orientation: tuple
+    fov: float
+    bg_start: tuple = DEFAULT_BG_START
+    bg_end: tuple = DEFAULT_BG_END
+    description: str = ""
+
+    def inputs(self) -> abi.InputStruct:
+        return camera_inputs(self.position, self.orientation, self.fov, bg_start=self.bg_start, bg_end=self.bg_end)
+
+    def scaled(self, width: int, height: int, spp: int | None = None) -> "Config":
+        c = Config(**{k: getattr(self, k) for k in self.__dataclass_fields__})
+        c.width, c.height = width, height
+        if spp is not None:
+            c.spp = spp
+        return c
+
+
+_RTIOW_FWD = normalized((-13.0, -2.0, -3.0))
+_TEX_FWD = normalized((0.0, -0.2, -1.0))
+
+# BASELINE.json "configs" 
+CONFIGS = {
+    "c1": Config("c1", SCENE_THREE_SPHERES, 400, 225, 4, 4, (0.0, 0.0, 1.0), (0.0, 0.0, -1.0), 45.0,
+                 description="400x225, 4 spp, depth 4, 3-sphere Lambertian scene (CPU reference path)"),
+    "c2": Config("c2", SCENE_RTIOW, 1920, 1080, 64, 8, (13.0, 2.0, 3.0), _RTIOW_FWD, 20.0,
+                 description="1920x1080, 64 spp, depth 8, RTIOW final random-spheres scene"),
+    "c3": Config("c3", SCENE_CORNELL, 3840, 2160, 256, 16, (278.0, 278.0, -800.0), (0.0, 0.0, 1.0), 40.0,
+                 bg_start=(0.0, 0.0, 0.0), bg_end=(0.0, 0.0, 0.0),
+                 description="3840x2160, 256 spp, depth 16, Cornell-box-style emissive scene"),
+    "c4": Config("c4", SCENE_RTIOW, 7680, 4320, 128, 8, (13.0, 2.0, 3.0), _RTIOW_FWD, 20.0,
+                 description="8 GPUs, 7680x4320, 128 spp, depth 8, RTIOW (image-tile split + gather)"),
+    "c5": Config("c5", SCENE_TEXTURED, 1920, 1080, 1, 4, (0.0, 2.0, 10.0), _TEX_FWD, 45.0,
+                 description="1920x1080, 1 spp progressive, depth 4, textured spheres + moving camera"),
+    "default": Config("default", SCENE_DEFAULT_WORLD, 800, 600, 36, 12, (0.0, 2.0, 12.0), (0.0, 0.0, -1.0), 45.0,
+                      description="the reference viewer's startup state (CudaLayer.h:66-67, 123-124)"),
+}
+
+
+def moving_camera(frame: int, frames: int = 60) -> tuple:
+    """C5's scripted camera path: an orbit around the scene (position, orientation)."""
+    ang = 2.0 * np.pi * frame / max(1, frames)
+    pos = (float(10.0 * np.sin(ang)), 2.0, float(10.0 * np.cos(ang)))
+    fwd = normalized((-pos[0], -1.5, -pos[2]))
+    return pos, fwd

@@ -1,0 +1,293 @@
+/*
+ * rt_hip.h — C ABI of librt_hip.so, the MI355X (gfx950) per-pixel path-tracing kernel.
+ *
+ * This header is the drop-in boundary for the hot path of Trippasch/CudaRayTracer.  The reference binds
+ * its render kernel through three extern "C" launchers compiled in CudaRayTracer/src/Cuda/Kernel.cu:178-204
+ * and declared by the caller in CudaRayTracer/src/Cuda/CudaLayer.cpp:12-19.  Every entry point below names
+ * the reference interface it replaces.  Only plain C types cross the boundary (no torch / HIP C++ types);
+ * `rt_stream` is an opaque hipStream_t (NULL = the legacy default stream).
+ *
+ * Conventions:
+ *   - rt_* functions return 0 on success or a negative rt_status; they never exit the process.
+ *     The message of the last failure on the calling thread is available from rt_last_error().
+ *   - The caller owns framebuffers and RNG-state buffers (device pointers).  The library owns the
+ *     device-side scene tables behind an rt_scene handle.
+ *   - rt_* launches are asynchronous on the given stream; the reference-named launchers are synchronous
+ *     (they end in a device synchronize, as Kernel.cu:190/196/203 do).
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Status codes                                                                                     */
+/* ------------------------------------------------------------------------------------------------ */
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARGUMENT = -1,
+    RT_ERR_INVALID_SCENE = -2,
+    RT_ERR_OUT_OF_MEMORY = -3,
+    RT_ERR_DEVICE = -4,        /* a HIP runtime call failed (message holds hipGetErrorString) */
+    RT_ERR_LAUNCH = -5,        /* hipGetLastError() after a kernel launch was not hipSuccess */
+    RT_ERR_UNSUPPORTED = -6
+} rt_status;
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Scene data model (flat).  Mirrors the reference's pointer graph:                                 */
+/*   Hittable{type,isActive,Object->{Sphere|XYRect|XZRect|YZRect}}   Hittables/Hittable.cuh:30-294   */
+/*   Material{type,Object->{Lambertian|Metal|Dielectric|DiffuseLight}} Hittables/Material.cuh:6-177 */
+/*   Texture{type,Object->{Constant|Checker|Image}}                    Hittables/Texture.cuh:6-109   */
+/* ------------------------------------------------------------------------------------------------ */
+typedef enum rt_hittable_type { /* HittableType, Hittable.cuh:30-38 (same numeric values) */
+    RT_SPHERE = 0,
+    RT_XYRECT = 1,
+    RT_XZRECT = 2,
+    RT_YZRECT = 3
+} rt_hittable_type;
+
+typedef enum rt_material_type { /* MaterialType, Material.cuh:6-12 */
+    RT_LAMBERTIAN = 0,
+    RT_METAL = 1,
+    RT_DIELECTRIC = 2,
+    RT_DIFFUSELIGHT = 3
+} rt_material_type;
+
+typedef enum rt_texture_type { /* TextureType, Texture.cuh:6-10 */
+    RT_CONSTANT = 0,
+    RT_CHECKER = 1,
+    RT_IMAGE = 2
+} rt_texture_type;
+
+typedef struct rt_texture_desc {
+    int32_t type;      /* rt_texture_type */
+    int32_t image;     /* RT_IMAGE: index into rt_scene_desc.images, or -1 for "no data" (Texture.cuh:83-84) */
+    float color[3];    /* RT_CONSTANT: Constant::color; RT_CHECKER: odd colour (Texture.cuh:58-67) */
+    float color2[3];   /* RT_CHECKER: even colour */
+} rt_texture_desc;     /* 32 B */
+
+typedef struct rt_material_desc {
+    int32_t type;            /* rt_material_type */
+    float fuzz;              /* RT_METAL: Metal::fuzz as the kernel reads it (ctor clamp Material.cuh:71 is the caller's) */
+    float ir;                /* RT_DIELECTRIC: Dielectric::ir */
+    int32_t light_intensity; /* RT_DIFFUSELIGHT: DiffuseLight::light_intensity (an int, Material.cuh:152) */
+    rt_texture_desc albedo;  /* Lambertian/Metal/DiffuseLight albedo texture */
+} rt_material_desc;          /* 48 B */
+
+typedef struct rt_hittable_desc {
+    int32_t type;      /* rt_hittable_type */
+    int32_t is_active; /* Hittable::isActive — inactive entries are dropped (Hittable.cuh:311-312) */
+    float center[3];   /* Sphere::center / *Rect::center */
+    float radius;      /* RT_SPHERE */
+    float width;       /* rects: XY width along x, XZ width along x, YZ width along z (Hittable.cuh:255-258) */
+    float height;      /* rects: XY height along y, XZ height along z, YZ height along y */
+    int32_t material;  /* index into rt_scene_desc.materials */
+    int32_t reserved;
+} rt_hittable_desc;    /* 40 B */
+
+typedef struct rt_image_desc {
+    const uint8_t* data; /* host pointer, RGB8, 3 bytes per texel, row-major (Texture.cuh:76, RawStbImage.h:13) */
+    int32_t width;
+    int32_t height;
+} rt_image_desc;
+
+typedef struct rt_scene_desc {
+    const rt_hittable_desc* hittables; /* in list order (m_List, CudaLayer.cpp:131) */
+    uint32_t num_hittables;
+    const rt_material_desc* materials;
+    uint32_t num_materials;
+    const rt_image_desc* images;
+    uint32_t num_images;
+} rt_scene_desc;
+
+/* InputStruct (Utils/SharedStructs.h:3-24): 18 floats, 72 B, same layout. */
+typedef struct rt_input_struct {
+    float origin[3];
+    float orientation[3];
+    float up[3];
+    float far_plane;
+    float near_plane;
+    float fov; /* radians (CudaLayer.cpp:62) */
+    float background_start[3];
+    float background_end[3];
+} rt_input_struct;
+
+/* curandStateXORWOW layout (48 B).  The caller allocates W·H of these exactly as CudaLayer.cpp:72 does
+ * (cudaMalloc(W·H·sizeof(curandState))); only d and v[5] are read or written by the kernel. */
+typedef struct rt_curand_state {
+    uint32_t d;
+    uint32_t v[5];
+    int32_t boxmuller_flag;
+    int32_t boxmuller_flag_double;
+    float boxmuller_extra;
+    uint32_t pad_;
+    double boxmuller_extra_double;
+} rt_curand_state;
+
+typedef struct rt_dim3 { /* binary-compatible with HIP/CUDA dim3 passed by value */
+    uint32_t x, y, z;
+} rt_dim3;
+
+typedef struct rt_scene rt_scene; /* opaque: device-resident flat scene (BVH + primitive + material tables) */
+typedef void* rt_stream;          /* hipStream_t */
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Reference-named drop-in launchers (same names, argument meaning, synchronous, void return).      */
+/* ------------------------------------------------------------------------------------------------ */
+
+/* Replaces `extern "C" void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int
+ * image_height, const unsigned int samples_per_pixel, const unsigned int max_depth, Hittable* world,
+ * curandState* d_rand_state, InputStruct inputs)` — Kernel.cu:178-191.
+ * `world` is the reference's Hittable* scene graph (see rt_reference_graph.h); it is re-flattened on
+ * every call because the viewer mutates it in place.  Floor-division grid as in
+ * Kernel.cu:184: pixels outside the last whole 16×16 block are not written.  Errors: rt_last_error(). */
+void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int image_height,
+                  const unsigned int samples_per_pixel, const unsigned int max_depth, const void* world,
+                  rt_curand_state* d_rand_state, rt_input_struct inputs);
+
+/* Replaces `extern "C" void LaunchRandInit(curandState* d_rand_state2)` — Kernel.cu:193-197
+ * (curand_init(1984, 0, 0) of one state). */
+void LaunchRandInit(rt_curand_state* d_rand_state2);
+
+/* Replaces `extern "C" void LaunchRenderInit(dim3 grid, dim3 block, unsigned int window_width,
+ * unsigned int window_height, curandState* d_rand_state)` — Kernel.cu:199-204: curand_init(1984 +
+ * pixel_index, 0, 0) for every thread (i, j) = threadIdx + blockIdx·blockDim of the given grid. */
+void LaunchRenderInit(rt_dim3 grid, rt_dim3 block, unsigned int window_width, unsigned int window_height,
+                      rt_curand_state* d_rand_state);
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Native API                                                                                       */
+/* ------------------------------------------------------------------------------------------------ */
+
+/* Last error message of the calling thread ("" if none). */
+const char* rt_last_error(void);
+
+/* Library version string. */
+const char* rt_version(void);
+
+/* hipSetDevice on the calling thread. */
+int rt_set_device(int device);
+
+/* Upload a flat scene: validates, drops inactive hittables, builds a binned-SAH BVH on the host and
+ * copies the tables to the current device.  Replaces the managed-memory pointer graph of
+ * CudaLayer::GenerateWorld (CudaLayer.cpp:103-256) + BVHNode ctor (Hittable.cuh:303-385). */
+int rt_scene_create(const rt_scene_desc* desc, rt_scene** out_scene);
+
+/* Re-read the scene from the reference's Hittable* graph (host-visible memory) — see
+ * rt_reference_graph.h — into a new rt_scene. */
+int rt_scene_from_reference_graph(const void* world, rt_scene** out_scene);
+
+/* Replace materials/textures in place (no BVH rebuild), like the viewer's material edits
+ * (CudaLayer.cpp:719-872).  num_materials must equal the scene's material count. */
+int rt_scene_update_materials(rt_scene* scene, const rt_material_desc* materials, uint32_t num_materials);
+
+int rt_scene_destroy(rt_scene* scene);
+
+typedef struct rt_scene_info {
+    uint32_t num_primitives; /* active hittables */
+    uint32_t num_nodes;      /* BVH nodes */
+    uint32_t num_materials;
+    uint32_t bvh_depth;
+    uint64_t device_bytes;   /* bytes of device tables */
+} rt_scene_info;
+int rt_scene_get_info(const rt_scene* scene, rt_scene_info* info);
+
+/* Row mapping of a (possibly tiled) render.  Local row l of the caller's buffers is global image row
+ *   g = ((l / band_rows) * num_ranks + rank) * band_rows + (l % band_rows)
+ * (block-cyclic row bands).  {band_rows = H, num_ranks = 1, rank = 0} is the whole
+ * image.  Pixel index for RNG seeding and the camera is always the GLOBAL g·W + x (Kernel.cu:119,175). */
+typedef struct rt_tiling {
+    uint32_t band_rows;
+    uint32_t num_ranks;
+    uint32_t rank;
+    uint32_t local_rows; /* rows held by the local buffers */
+} rt_tiling;
+
+/* curand_init(seed_base + global_pixel_index, 0, 0) for every local pixel (Kernel.cu:166-176). */
+int rt_render_init(rt_curand_state* d_state, uint32_t width, uint32_t height, const rt_tiling* tiling,
+                   uint64_t seed_base, rt_stream stream);
+
+enum rt_render_flags {
+    RT_FLAG_FAITHFUL_GRID = 1u << 0, /* skip pixels outside whole 16×16 blocks (Kernel.cu:184) */
+    RT_FLAG_NO_STATE_WRITEBACK = 1u << 1, /* do not store the advanced RNG state (benchmark repeatability) */
+    RT_FLAG_ACCUMULATE = 1u << 2, /* accum[px].rgb += Σ samples, accum[px].w += spp; pos shows rgb / w */
+    RT_FLAG_RIUS_LEFT_TO_RIGHT = 1u << 3, /* fill Random()'s Vec3(ξ,ξ,ξ) left to right (default: right to
+                                             left, the order the survey's g++ build of Math.cuh:233 used) */
+    RT_FLAG_COUNT_TESTS = 1u << 4 /* also count box and primitive tests into counters[1], [2] */
+};
+
+typedef struct rt_render_args {
+    uint32_t* pos;            /* device RGBA8 framebuffer, local_rows × width (may be NULL if accum given) */
+    float* radiance;          /* optional device float[local_rows·width·4]: pre-gamma mean colour (col/spp) */
+    float* accum;             /* RT_FLAG_ACCUMULATE: device float4 running sum of samples */
+    rt_curand_state* state;   /* device RNG states, local_rows × width */
+    uint64_t* counters;       /* optional device uint64[4]: rays, box tests, primitive tests, primary */
+    uint32_t width;
+    uint32_t height;          /* global image height */
+    uint32_t samples_per_pixel;
+    uint32_t max_depth;
+    uint32_t flags;           /* rt_render_flags */
+    uint32_t reserved;        /* must be 0 */
+    rt_tiling tiling;
+    rt_input_struct inputs;
+} rt_render_args;
+
+/* One frame of the per-pixel render kernel (Kernel.cu:102-158) on `stream`. */
+int rt_render(const rt_scene* scene, const rt_render_args* args, rt_stream stream);
+
+/* Kernel duration of the last rt_render on this thread measured with HIP events on its stream
+ * (milliseconds); requires rt_set_timing(1) before the launch.  Returns <0 when unavailable. */
+int rt_set_timing(int enabled);
+float rt_last_kernel_ms(void);
+
+/* Tuning/benchmark knob (per thread): -1 = automatic; 0..5 = (scene tables staged in LDS) * 3 + traversal
+ * stack kind (0 = scratch, 1 = LDS, 2 = 4 VGPRs + scratch).  Returns the previous value. */
+int rt_set_variant(int variant);
+
+/* Host-side helpers (no device needed). */
+
+/* Flatten the reference's Hittable* graph (rt_reference_graph.h) into flat arrays (size query with NULL
+ * arrays; counts are in/out).  This is the host step of rt_scene_from_reference_graph / LaunchKernel. */
+int rt_reference_graph_flatten(const void* world, rt_hittable_desc* hittables, uint32_t* num_hittables,
+                               rt_material_desc* materials, uint32_t* num_materials, rt_image_desc* images,
+                               uint32_t* num_images);
+
+/* Build the device tables on the host only and copy them out (for inspection/tests): nodes 16 floats,
+ * prims 8 floats, materials 12 floats each; prim_source[i] = hittable index of primitive i.  Size query
+ * with NULL arrays. */
+typedef struct rt_host_tables_info {
+    uint32_t num_nodes, num_prims, num_materials, depth;
+} rt_host_tables_info;
+int rt_build_host_tables(const rt_scene_desc* desc, float* nodes, float* prims, float* materials,
+                         int32_t* prim_source, rt_host_tables_info* info);
+
+/* glibc random_r TYPE_3 restatement: rand() sequence after srand(seed) (RND macro, Math.cuh:12). */
+typedef struct rt_glibc_rand { int32_t r[34]; uint32_t idx; } rt_glibc_rand;
+void rt_glibc_srand(rt_glibc_rand* g, uint32_t seed);
+int32_t rt_glibc_rand_next(rt_glibc_rand* g);
+
+/* Built-in scenes, written into caller-provided arrays (query sizes with NULL arrays).
+ *   0 = CudaLayer::GenerateWorld default world (CudaLayer.cpp:103-256): XZ checker ground + 16 spheres
+ *   1 = 3-sphere Lambertian scene (BASELINE config 1)
+ *   2 = RTIOW book-1 final random-spheres scene in the reference's types (BASELINE config 2/4)
+ *   3 = Cornell-style emissive box of XY/XZ/YZ rects (BASELINE config 3)
+ *   4 = textured spheres (BASELINE config 5); image 0 is a procedural RGB8 texture
+ * `seed` seeds rt_glibc_srand for the scenes that draw random numbers (glibc default is 1). */
+int rt_builtin_scene(int which, uint32_t seed, rt_hittable_desc* hittables, uint32_t* num_hittables,
+                     rt_material_desc* materials, uint32_t* num_materials);
+
+/* Camera → InputStruct exactly as CudaLayer.cpp:43-65: up = normalize(cross(o, normalize(cross(o, up0)))). */
+void rt_camera_inputs(const float position[3], const float orientation[3], const float world_up[3],
+                      float fov_degrees, float near_plane, float far_plane, const float bg_start[3],
+                      const float bg_end[3], rt_input_struct* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_HIP_H */

@@ -1,0 +1,79 @@
+"""Regenerate the golden fixtures in tests/golden/ from the CPU oracle (oracle/rt_oracle.c).
+
+    python tests/golden/make_golden.py
+
+Inputs are the built-in scenes of librt_hip.so's host code (csrc/builtin_scenes.cpp; no device needed) and
+the BASELINE configurations of cudaraytracer_amd/scenes.py; outputs are the oracle's RGBA8 images, RNG
+states after the frame and ray/test counters.  Scene tables are stored too, so a change of the scene
+generators shows up as a fixture mismatch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+
+from cases import CASES  # noqa: E402
+from cudaraytracer_amd import abi, scenes  # noqa: E402
+from oracle import py_oracle as po  # noqa: E402
+
+
+def xorwow_kat() -> dict:
+    out = {}
+    for seed in (0, 1, 1984, 1985, 1984 + 1919, (1 << 32) + 7, 2**63 + 12345):
+        st = abi.CurandState()
+        po.lib().orc_curand_init(seed, C.byref(st))
+        init = [st.d] + list(st.v)
+        raw = [po.lib().orc_curand(C.byref(st)) for _ in range(8)]
+        po.lib().orc_curand_init(seed, C.byref(st))
+        uni = [float(po.lib().orc_curand_uniform(C.byref(st))) for _ in range(8)]
+        out[str(seed)] = {"init": init, "raw": raw, "uniform": uni}
+    return out
+
+
+def digest(a: np.ndarray) -> bytes:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest()
+
+
+def main() -> None:
+    with open(os.path.join(HERE, "xorwow_kat.json"), "w") as f:
+        json.dump(xorwow_kat(), f, indent=1)
+    for which in range(5):
+        s = scenes.builtin(which)
+        np.savez_compressed(os.path.join(HERE, f"scene_{which}.npz"),
+                            hittables=np.frombuffer(s.hittables_bytes(), np.uint8),
+                            materials=np.frombuffer(s.materials_bytes(), np.uint8))
+    for case in CASES:
+        cfg = case.cfg()
+        sc = scenes.builtin(cfg.scene)
+        osc = po.OracleScene(sc)
+        inp = cfg.inputs()
+        st = po.init_states(cfg.width, cfg.height, full=not case.faithful_grid)
+        st0 = st.copy()
+        pos, rad, cnt = po.render(osc, cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st,
+                                  faithful_grid=case.faithful_grid, rius_order=case.rius_order, radiance=True)
+        np.savez_compressed(
+            os.path.join(HERE, f"{case.name}.npz"),
+            inputs=np.frombuffer(bytes(inp), np.uint8),
+            pos=pos,
+            # RNG words d, v[0..4] are incompressible: keep digests (tests recompute them)
+            state_before_sha256=np.frombuffer(digest(st0[:, :6]), np.uint8),
+            state_after_sha256=np.frombuffer(digest(st[:, :6]), np.uint8),
+            radiance_sha256=np.frombuffer(digest(rad), np.uint8),
+            counters=np.array([cnt.rays, cnt.box_tests, cnt.prim_tests, cnt.primary], np.uint64),
+            texture_sha256=np.frombuffer(digest(np.asarray(sc.images[0]) if sc.images else np.zeros(0, np.uint8)),
+                                         np.uint8))
+        print(case.name, pos.shape, cnt.rays, flush=True)
+
+
+if __name__ == "__main__":
+    main()

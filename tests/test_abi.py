@@ -1,0 +1,57 @@
+"""CPU tests of the C-ABI boundary: librt_hip.so loads, exports every function include/*.h declares, and the
+struct layouts match the reference's (InputStruct 72 B, curandState 48 B, graph node sizes)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+from cudaraytracer_amd import abi
+from cudaraytracer_amd._lib import EXPORTED, LIB_PATH, lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions() -> set:
+    names = set()
+    for fn in os.listdir(os.path.join(ROOT, "include")):
+        if not fn.endswith(".h"):
+            continue
+        text = open(os.path.join(ROOT, "include", fn)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", text, flags=re.M):
+            name = m.group(1)
+            if name not in {"if", "sizeof", "static_assert", "typedef"}:
+                names.add(name)
+    return names
+
+
+def test_library_loads():
+    assert os.path.exists(LIB_PATH)
+    assert lib().rt_version().startswith(b"librt_hip")
+
+
+def test_every_declared_symbol_is_exported():
+    decl = declared_functions()
+    assert decl == set(EXPORTED), (decl ^ set(EXPORTED))
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = decl - exported
+    assert not missing, missing
+    for name in decl:
+        assert hasattr(lib(), name)
+
+
+def test_struct_layouts():
+    assert C.sizeof(abi.InputStruct) == 72  # SharedStructs.h:3-24
+    assert C.sizeof(abi.CurandState) == 48  # curandStateXORWOW
+    assert C.sizeof(abi.Dim3) == 12
+    assert C.sizeof(abi.HittableDesc) == 40 and C.sizeof(abi.MaterialDesc) == 48
+
+
+def test_error_reporting_without_device():
+    h = C.c_void_p()
+    assert lib().rt_scene_create(None, C.byref(h)) == -1
+    assert b"NULL" in lib().rt_last_error()
+    assert lib().rt_render(None, None, None) == -1

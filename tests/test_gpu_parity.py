@@ -1,0 +1,330 @@
+"""GPU parity tests (MI355X): librt_hip.so through the C ABI against the oracle and the golden fixtures.
+
+Bar: the RGBA8 image, the advanced cuRAND states and the ray count are BIT-EXACT with the oracle on every
+golden case and kernel variant (the arithmetic contract in render.hip).  Full-size configurations are
+checked through size-independent properties (tile invariance, determinism, equality of row samples with the
+oracle, radiance/pos consistency).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import refgraph
+from cases import CASE_BY_NAME, CASES
+from cudaraytracer_amd import abi, scenes
+from cudaraytracer_amd._lib import RTError, lib
+from cudaraytracer_amd.renderer import DeviceScene, Renderer
+from helpers import digest, image_stats, load_golden
+from oracle import py_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [0, 1, 2, 3, 4, 5]
+
+
+@pytest.fixture(autouse=True)
+def _variant_reset():
+    yield
+    lib().rt_set_variant(-1)
+
+
+def _render(case, variant=-1, radiance=False, count_tests=False):
+    cfg = case.cfg()
+    lib().rt_set_variant(variant)
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    sc = scenes.builtin(cfg.scene)
+    ds = DeviceScene(sc)
+    flags = case.flags | (abi.RT_FLAG_COUNT_TESTS if count_tests else 0)
+    if case.faithful_grid:
+        # the reference's RenderInit only seeds the floor grid; seed the same way (LaunchRenderInit)
+        r.state.zero_()
+        grid = abi.Dim3(cfg.width // 16, cfg.height // 16, 1)
+        lib().LaunchRenderInit(grid, abi.Dim3(16, 16, 1), cfg.width, cfg.height, C.c_void_p(r.state.data_ptr()))
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=flags, radiance=radiance)
+    torch.cuda.synchronize()
+    return r, ds, sc
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c.name)
+def test_bit_exact_vs_golden(case, variant):
+    g = load_golden(case.name)
+    r, _, _ = _render(case, variant)
+    img = r.image()
+    assert image_stats(img, g["pos"])["exact"] == 1.0, image_stats(img, g["pos"])
+    np.testing.assert_array_equal(img, g["pos"])
+    assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes()
+    assert int(r.counters[0]) == int(g["counters"][0])  # rays
+    assert int(r.counters[3]) == int(g["counters"][3])  # primary samples
+
+
+@pytest.mark.parametrize("case", [CASE_BY_NAME["c2_rtiow_192x112_s16"], CASE_BY_NAME["c3_cornell_128_s16"]],
+                         ids=lambda c: c.name)
+def test_radiance_matches_oracle(case):
+    cfg = case.cfg()
+    r, _, sc = _render(case, radiance=True)
+    st = po.init_states(cfg.width, cfg.height)
+    _, rad, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                          radiance=True, rius_order=case.rius_order)
+    np.testing.assert_array_equal(r.radiance_image(), rad)
+    # pos is the gamma-2 RGBA8 of the radiance (Kernel.cu:151-157)
+    c = np.clip(255.0 * np.sqrt(rad[..., :3].astype(np.float32)), 0, 255).astype(np.uint32)
+    assert np.array_equal(r.image() & 0xFFFFFF, c[..., 0] | (c[..., 1] << 8) | (c[..., 2] << 16))
+
+
+def test_count_tests_flag_does_not_change_the_image():
+    case = CASE_BY_NAME["c2_rtiow_192x112_s16"]
+    r, _, _ = _render(case, count_tests=True)
+    g = load_golden(case.name)
+    np.testing.assert_array_equal(r.image(), g["pos"])
+    rays, boxes, prims = (int(x) for x in r.counters[:3])
+    assert boxes > 2 * rays and prims > 0
+
+
+@pytest.mark.parametrize("num_ranks, band_rows", [(2, 16), (3, 16), (4, 8), (8, 16)])
+def test_tile_split_is_bit_identical(num_ranks, band_rows):
+    """N-rank block-cyclic bands reassemble into exactly the 1-rank image (global-index RNG seeding)."""
+    case = CASE_BY_NAME["c2_rtiow_192x112_s16"]
+    cfg = case.cfg()
+    g = load_golden(case.name)
+    sc = scenes.builtin(cfg.scene)
+    ds = DeviceScene(sc)
+    full = np.zeros((cfg.height, cfg.width), np.uint32)
+    rays = 0
+    for rank in range(num_ranks):
+        r = Renderer(cfg.width, cfg.height, band_rows=band_rows, num_ranks=num_ranks, rank=rank)
+        r.render_init()
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+        torch.cuda.synchronize()
+        full[r.rows] = r.image()
+        rays += int(r.counters[0])
+    np.testing.assert_array_equal(full, g["pos"])
+    assert rays == int(g["counters"][0])
+
+
+def test_faithful_grid_leaves_partial_blocks_untouched():
+    case = CASE_BY_NAME["c1_full"]
+    cfg = case.cfg()
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    r.pos.fill_(0x12345678)
+    ds = DeviceScene(scenes.builtin(cfg.scene))
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_FAITHFUL_GRID)
+    torch.cuda.synchronize()
+    img = r.image()
+    assert np.all(img[224] == 0x12345678)  # 225 rows → 14 whole 16-row blocks (Kernel.cu:184)
+    assert np.all(img[:224] != 0x12345678)
+
+
+def test_drop_in_launchers_match_oracle():
+    """LaunchRenderInit / LaunchRandInit / LaunchKernel(world graph) against the oracle (Kernel.cu:178-204)."""
+    case = CASE_BY_NAME["default_world_160x120_s8"]
+    cfg = case.cfg()
+    sc = scenes.builtin(cfg.scene)
+    dev = torch.device("cuda", 0)
+    W, H = cfg.width, cfg.height
+    pos = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    state = torch.zeros(W * H * abi.STATE_WORDS, dtype=torch.int32, device=dev)
+    state2 = torch.zeros(abi.STATE_WORDS, dtype=torch.int32, device=dev)
+    lib().LaunchRandInit(C.c_void_p(state2.data_ptr()))
+    lib().LaunchRenderInit(abi.Dim3(W // 16, H // 16, 1), abi.Dim3(16, 16, 1), W, H, C.c_void_p(state.data_ptr()))
+    ref_state = po.init_states(W, H, full=False)
+    got_state = state.cpu().numpy().view(np.uint32).reshape(-1, abi.STATE_WORDS)
+    np.testing.assert_array_equal(got_state, ref_state)
+    kat = abi.CurandState()
+    po.lib().orc_curand_init(1984, C.byref(kat))
+    assert state2.cpu().numpy().view(np.uint32).tobytes() == bytes(kat)
+    graph = refgraph.build_graph(sc)
+    lib().LaunchKernel(C.c_void_p(pos.data_ptr()), W, H, cfg.spp, cfg.depth, C.c_void_p(C.addressof(graph.world)),
+                       C.c_void_p(state.data_ptr()), cfg.inputs())
+    ref, _, _ = po.render(po.OracleScene(sc), W, H, cfg.spp, cfg.depth, cfg.inputs(), ref_state, faithful_grid=True)
+    np.testing.assert_array_equal(pos.cpu().numpy().view(np.uint32).reshape(H, W), ref)
+    # a material edit in place (CudaLayer.cpp:839-843) is picked up by the next launch without a rebuild
+    m = graph.keep[[i for i, o in enumerate(graph.keep) if isinstance(o, refgraph.Constant)][1]]
+    m.color.e[0] = 0.0
+    lib().LaunchKernel(C.c_void_p(pos.data_ptr()), W, H, cfg.spp, cfg.depth, C.c_void_p(C.addressof(graph.world)),
+                       C.c_void_p(state.data_ptr()), cfg.inputs())
+    nh, nm, ni = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
+    world = C.addressof(graph.world)
+    lib().rt_reference_graph_flatten(world, None, C.byref(nh), None, C.byref(nm), None, C.byref(ni))
+    h = (abi.HittableDesc * nh.value)()
+    mm = (abi.MaterialDesc * nm.value)()
+    im = (abi.ImageDesc * 1)()
+    lib().rt_reference_graph_flatten(world, h, C.byref(nh), mm, C.byref(nm), im, C.byref(ni))
+    edited = scenes.Scene(h, mm, [])
+    ref2, _, _ = po.render(po.OracleScene(edited), W, H, cfg.spp, cfg.depth, cfg.inputs(), ref_state, faithful_grid=True)
+    np.testing.assert_array_equal(pos.cpu().numpy().view(np.uint32).reshape(H, W), ref2)
+
+
+def test_material_update_without_rebuild():
+    case = CASE_BY_NAME["c2_rtiow_ragged_100x37_s4"]
+    cfg = case.cfg()
+    sc = scenes.builtin(cfg.scene)
+    ds = DeviceScene(sc)
+    for i in range(len(sc.materials)):
+        if sc.materials[i].type == abi.RT_LAMBERTIAN:
+            sc.materials[i].albedo.color[:] = [0.9, 0.1, 0.1]
+    ds.update_materials(sc.materials)
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
+    np.testing.assert_array_equal(r.image(), ref)
+
+
+def test_edge_cases_spp0_depth0_empty_and_inactive():
+    cfg = scenes.CONFIGS["c2"].scaled(48, 32, 3)
+    sc = scenes.builtin(cfg.scene)
+    ds = DeviceScene(sc)
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    before = r.states().copy()
+    r.render(ds, 0, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    assert np.all(r.image() == 0xFF000000)  # col/0 = NaN → int(NaN) = 0
+    np.testing.assert_array_equal(r.states(), before)
+    r.render(ds, 2, 0, cfg.inputs())  # max_depth 0: black, 2 draws per sample
+    torch.cuda.synchronize()
+    assert np.all(r.image() == 0xFF000000) and int(r.counters[0]) == 0
+    ref_st = po.init_states(cfg.width, cfg.height)
+    for i in range(ref_st.shape[0]):
+        s = abi.CurandState.from_buffer(ref_st[i])
+        for _ in range(4):
+            po.lib().orc_curand(C.byref(s))
+    np.testing.assert_array_equal(r.states()[:, :6], ref_st[:, :6])
+    # all hittables inactive → empty scene → pure sky; some inactive → oracle with the same flags
+    for k in range(sc.num_hittables):
+        sc.hittables[k].is_active = 1 if k % 3 else 0
+    ds2 = DeviceScene(sc)
+    r2 = Renderer(cfg.width, cfg.height)
+    r2.render_init()
+    r2.render(ds2, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
+    np.testing.assert_array_equal(r2.image(), ref)
+    for k in range(sc.num_hittables):
+        sc.hittables[k].is_active = 0
+    ds3 = DeviceScene(sc)
+    r3 = Renderer(cfg.width, cfg.height)
+    r3.render_init()
+    r3.render(ds3, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
+    np.testing.assert_array_equal(r3.image(), ref)
+    assert int(r3.counters[0]) == cnt.rays == cfg.width * cfg.height * cfg.spp
+
+
+def test_single_primitive_scene():
+    cfg = scenes.CONFIGS["c1"].scaled(64, 36, 4)
+    sc = scenes.builtin(cfg.scene)
+    sc.hittables[0].is_active = 0
+    sc.hittables[2].is_active = 0
+    ds = DeviceScene(sc)
+    assert ds.info().num_primitives == 1
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
+    np.testing.assert_array_equal(r.image(), ref)
+
+
+def test_accumulate_first_frame_equals_plain_frame():
+    case = CASE_BY_NAME["c5_textured_160x96_s4"]
+    cfg = case.cfg()
+    g = load_golden(case.name)
+    ds = DeviceScene(scenes.builtin(cfg.scene))
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_ACCUMULATE)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r.image(), g["pos"])
+    acc1 = r.accum.cpu().numpy().reshape(-1, 4).copy()
+    assert np.all(acc1[:, 3] == cfg.spp)
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_ACCUMULATE)
+    torch.cuda.synchronize()
+    acc2 = r.accum.cpu().numpy().reshape(-1, 4)
+    assert np.all(acc2[:, 3] == 2 * cfg.spp) and np.all(acc2[:, :3] >= acc1[:, :3])
+
+
+def test_invalid_arguments_fail_loudly():
+    cfg = scenes.CONFIGS["c1"].scaled(32, 16, 1)
+    r = Renderer(cfg.width, cfg.height)
+    ds = DeviceScene(scenes.builtin(cfg.scene))
+    r.num_ranks, r.rank = 2, 5  # rank outside the tiling
+    with pytest.raises(RTError, match="tiling"):
+        r.render(ds, 1, 1, cfg.inputs())
+    a = abi.RenderArgs()
+    a.pos, a.width, a.height = r.pos.data_ptr(), 32, 16
+    assert lib().rt_render(ds.handle, C.byref(a), None) == -1  # NULL state
+    assert b"state" in lib().rt_last_error()
+
+
+# ---------------------------------------------------------------------------------------------------
+# Full-size configurations: size-independent properties
+# ---------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_full_size_rows_match_oracle_and_tiles_are_invariant(config):
+    cfg = scenes.CONFIGS[config]
+    if config == "c3":
+        cfg = cfg.scaled(cfg.width, cfg.height, 16)  # 256 spp × 8.3 Mpx is minutes of CPU oracle; rows still full-width
+    sc = scenes.builtin(cfg.scene)
+    ds = DeviceScene(sc)
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    img = r.image()
+    assert np.all((img >> 24) == 0xFF)
+    # oracle on a strided sample of full rows (same global pixel indices → same RNG streams)
+    step = cfg.height // 6
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                          rows=(1, cfg.height), row_step=step, threads=16)
+    rows = list(range(1, cfg.height, step))
+    np.testing.assert_array_equal(img[rows], ref[rows])
+    np.testing.assert_array_equal(r.states().reshape(cfg.height, cfg.width, -1)[rows, :, :6],
+                                  st.reshape(cfg.height, cfg.width, -1)[rows, :, :6])
+    # 4-rank band split of the full frame reassembles bit-identically
+    full = np.zeros_like(img)
+    for rank in range(4):
+        rr = Renderer(cfg.width, cfg.height, band_rows=16, num_ranks=4, rank=rank)
+        rr.render_init()
+        rr.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+        torch.cuda.synchronize()
+        full[rr.rows] = rr.image()
+        del rr
+    np.testing.assert_array_equal(full, img)
+
+
+def test_full_size_c2_determinism_and_frame_sequence():
+    cfg = scenes.CONFIGS["c2"]
+    ds = DeviceScene(scenes.builtin(cfg.scene))
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    s0 = r.state.clone()
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
+    torch.cuda.synchronize()
+    a = r.image().copy()
+    assert torch.equal(r.state, s0)
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    b = r.image().copy()
+    np.testing.assert_array_equal(a, b)
+    rays = int(r.counters[0]) // 2
+    assert 2.9 < rays / (cfg.width * cfg.height * cfg.spp) < 3.3  # ≈3.0-3.1 rays per primary
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())  # next frame continues the RNG streams (Kernel.cu:149)
+    torch.cuda.synchronize()
+    c = r.image()
+    s = image_stats(b, c)
+    assert s["exact"] < 0.9 and abs(s["mean_signed"]) < 0.5  # new noise, same expectation

@@ -1,0 +1,194 @@
+"""CPU tests of librt_hip.so's host code: scene generators, glibc rand restatement, camera set-up, scene
+validation, the BVH build and the reference-graph flattener (no device needed)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import refgraph
+from cudaraytracer_amd import abi, scenes
+from cudaraytracer_amd._lib import lib
+from helpers import load_golden
+
+
+def test_glibc_rand_restatement_matches_libc():
+    libc = C.CDLL("libc.so.6")
+    for seed in (1, 42, 1984):
+        g = abi.GlibcRand()
+        lib().rt_glibc_srand(C.byref(g), seed)
+        libc.srand(seed)
+        assert [lib().rt_glibc_rand_next(C.byref(g)) for _ in range(3000)] == [libc.rand() for _ in range(3000)]
+
+
+@pytest.mark.parametrize("which", range(5))
+def test_builtin_scenes_match_golden(which):
+    s = scenes.builtin(which)
+    g = load_golden(f"scene_{which}")
+    assert s.hittables_bytes() == g["hittables"].tobytes()
+    assert s.materials_bytes() == g["materials"].tobytes()
+
+
+def test_builtin_scene_shapes():
+    rtiow = scenes.builtin(scenes.SCENE_RTIOW)
+    assert rtiow.num_hittables == 488  # 1 ground + 22×22 + 3
+    kinds = [rtiow.materials[h.material].type for h in rtiow.hittables]
+    assert kinds.count(abi.RT_DIELECTRIC) >= 1 and kinds.count(abi.RT_METAL) >= 1
+    world = scenes.builtin(scenes.SCENE_DEFAULT_WORLD)
+    assert world.num_hittables == 17 and world.hittables[0].type == abi.RT_XZRECT
+    assert world.materials[0].albedo.type == abi.RT_CHECKER
+    for h in list(world.hittables)[1:]:
+        m = world.materials[h.material]
+        assert h.type == abi.RT_SPHERE
+        assert h.radius == pytest.approx({abi.RT_LAMBERTIAN: 0.2, abi.RT_METAL: 0.2, abi.RT_DIELECTRIC: 0.3,
+                                          abi.RT_DIFFUSELIGHT: 0.5}[m.type])
+        if m.type == abi.RT_METAL:
+            assert 0 <= m.fuzz <= 0.5
+    cornell = scenes.builtin(scenes.SCENE_CORNELL)
+    assert {h.type for h in cornell.hittables} == {abi.RT_XYRECT, abi.RT_XZRECT, abi.RT_YZRECT, abi.RT_SPHERE}
+
+
+def test_camera_inputs_reference_up_vector():
+    """CudaLayer.cpp:45-46 passes up = normalize(cross(o, normalize(cross(o, worldUp)))): down for a level camera."""
+    inp = scenes.camera_inputs((0.0, 2.0, 12.0), (0.0, 0.0, -1.0), 45.0)
+    assert list(inp.up) == [0.0, -1.0, 0.0]
+    assert inp.fov == pytest.approx(np.radians(45.0), rel=1e-7)
+    assert (inp.near_plane, inp.far_plane) == (pytest.approx(0.1), 10.0)
+    assert list(inp.background_start) == [1.0, 1.0, 1.0] and list(inp.background_end) == pytest.approx([0.5, 0.7, 1.0])
+    assert C.sizeof(inp) == 72
+
+
+def _tables(scene):
+    desc = scene.desc()
+    info = abi.HostTablesInfo()
+    assert lib().rt_build_host_tables(C.byref(desc), None, None, None, None, C.byref(info)) == 0
+    nodes = (C.c_float * (16 * info.num_nodes))()
+    prims = (C.c_float * (8 * info.num_prims))()
+    mats = (C.c_float * (12 * info.num_materials))()
+    src = (C.c_int32 * max(1, info.num_prims))()
+    assert lib().rt_build_host_tables(C.byref(desc), nodes, prims, mats, src, C.byref(info)) == 0
+    return (info, np.frombuffer(nodes, np.float32).reshape(-1, 16), np.frombuffer(prims, np.float32).reshape(-1, 8),
+            np.frombuffer(src, np.int32)[: info.num_prims])
+
+
+@pytest.mark.parametrize("which", range(5))
+def test_bvh_covers_every_active_primitive_once_with_conservative_boxes(which):
+    scene = scenes.builtin(which)
+    info, nodes, prims, src = _tables(scene)
+    active = [i for i in range(scene.num_hittables) if scene.hittables[i].is_active]
+    assert sorted(src.tolist()) == active
+    ints = nodes.view(np.int32)
+    seen = []
+
+    def prim_box(i):
+        h = scene.hittables[int(src[i])]
+        c = np.float32(h.center)
+        if h.type == abi.RT_SPHERE:
+            return c - np.float32(h.radius), c + np.float32(h.radius)
+        k = {abi.RT_XYRECT: 2, abi.RT_XZRECT: 1, abi.RT_YZRECT: 0}[h.type]
+        lo, hi = prims[i, [1, 3]], prims[i, [2, 4]]
+        axes = {2: (0, 1), 1: (0, 2), 0: (1, 2)}[k]
+        blo, bhi = np.zeros(3, np.float32), np.zeros(3, np.float32)
+        blo[list(axes)], bhi[list(axes)] = lo, hi
+        blo[k], bhi[k] = c[k] - np.float32(1e-4), c[k] + np.float32(1e-4)
+        return blo, bhi
+
+    def walk(child, lo, hi, depth):
+        assert depth <= info.depth
+        if child < 0:
+            leaf = ~child
+            first, count = leaf >> 4, leaf & 15
+            assert 1 <= count <= 4
+            for i in range(first, first + count):
+                seen.append(i)
+                plo, phi = prim_box(i)
+                assert np.all(lo < plo) and np.all(hi > phi), (lo, hi, plo, phi)  # strictly padded outward
+            return
+        n = nodes[child]
+        boxes = [(n[[0, 2, 8]], n[[1, 3, 9]]), (n[[4, 6, 10]], n[[5, 7, 11]])]
+        for k in range(2):
+            blo, bhi = boxes[k]
+            assert np.all(blo >= lo) and np.all(bhi <= hi)
+            walk(int(ints[child, 12 + k]), blo, bhi, depth + 1)
+
+    inf = np.float32(np.inf)
+    walk(0, np.full(3, -inf), np.full(3, inf), 1)
+    if info.num_prims == 1:
+        assert seen == [0, 0]
+    else:
+        assert sorted(seen) == list(range(info.num_prims))
+
+
+def test_bvh_is_shallow_and_small_for_rtiow():
+    info, nodes, _, _ = _tables(scenes.builtin(scenes.SCENE_RTIOW))
+    assert info.num_prims == 488 and info.depth <= 24
+    assert nodes.nbytes + info.num_prims * 32 <= 48 * 1024  # LDS-stageable
+
+
+def test_inactive_hittables_are_dropped():
+    s = scenes.builtin(scenes.SCENE_DEFAULT_WORLD)
+    s.hittables[3].is_active = 0
+    s.hittables[7].is_active = 0
+    _, _, _, src = _tables(s)
+    assert 3 not in src.tolist() and 7 not in src.tolist() and len(src) == 15
+
+
+def test_empty_and_single_primitive_scenes():
+    s = scenes.builtin(scenes.SCENE_THREE_SPHERES)
+    for h in s.hittables:
+        h.is_active = 0
+    info, _, _, _ = _tables(s)
+    assert info.num_nodes == 0 and info.num_prims == 0
+    s.hittables[1].is_active = 1
+    info, nodes, _, src = _tables(s)
+    assert info.num_nodes == 1 and src.tolist() == [1]
+
+
+@pytest.mark.parametrize("mutate, code", [
+    (lambda s: setattr(s.hittables[0], "material", 99), -2),
+    (lambda s: setattr(s.hittables[0], "type", 7), -2),
+    (lambda s: setattr(s.materials[0], "type", 9), -2),
+    (lambda s: setattr(s.materials[0].albedo, "type", 5), -2),
+])
+def test_invalid_scenes_are_rejected(mutate, code):
+    s = scenes.builtin(scenes.SCENE_THREE_SPHERES)
+    mutate(s)
+    desc = s.desc()
+    info = abi.HostTablesInfo()
+    assert lib().rt_build_host_tables(C.byref(desc), None, None, None, None, C.byref(info)) == code
+    assert lib().rt_last_error()
+    handle = C.c_void_p()
+    assert lib().rt_scene_create(C.byref(desc), C.byref(handle)) == code  # validation precedes any device call
+
+
+@pytest.mark.parametrize("which", [scenes.SCENE_DEFAULT_WORLD, scenes.SCENE_CORNELL, scenes.SCENE_TEXTURED])
+def test_reference_graph_flattens_to_the_same_scene(which):
+    s = scenes.builtin(which)
+    g = refgraph.build_graph(s)
+    nh, nm, ni = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
+    world = C.addressof(g.world)
+    assert lib().rt_reference_graph_flatten(world, None, C.byref(nh), None, C.byref(nm), None, C.byref(ni)) == 0
+    h = (abi.HittableDesc * nh.value)()
+    m = (abi.MaterialDesc * nm.value)()
+    im = (abi.ImageDesc * max(1, ni.value))()
+    assert lib().rt_reference_graph_flatten(world, h, C.byref(nh), m, C.byref(nm), im, C.byref(ni)) == 0
+    assert nh.value == s.num_hittables
+    # same primitives and materials (order may differ: the graph is walked in BVH order)
+    want = sorted((bytes(x.center), x.type, x.radius, x.width, x.height, bytes(s.materials[x.material]))
+                  for x in s.hittables)
+    got = []
+    for x in h:
+        mm = m[x.material]
+        if mm.albedo.type == abi.RT_IMAGE:
+            mm.albedo.image = 0  # one image per textured material in the graph
+        got.append((bytes(x.center), x.type, x.radius, x.width, x.height, bytes(mm)))
+    assert sorted(got) == want
+
+
+def test_reference_graph_rejects_non_bvh_world():
+    bad = refgraph.Hittable()
+    bad.type = abi.RT_SPHERE
+    nh, nm, ni = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
+    assert lib().rt_reference_graph_flatten(C.addressof(bad), None, C.byref(nh), None, C.byref(nm), None,
+                                            C.byref(ni)) == -2

@@ -1,0 +1,241 @@
+"""CPU tests of the oracle (oracle/rt_oracle.c): pinned against the survey-recorded reference values and the
+committed golden fixtures, plus analytical known-answer tests of each restated function."""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from cases import CASES
+from cudaraytracer_amd import abi, scenes
+from helpers import GOLDEN, digest, load_golden
+from oracle import py_oracle as po
+
+pytestmark = pytest.mark.filterwarnings("ignore")
+
+
+# ---------------------------------------------------------------------------------------------------
+# Pins from SURVEY.md §8(c) C1 / §6 (outputs of the reference's own hot-path source, survey probe)
+# ---------------------------------------------------------------------------------------------------
+def test_xorwow_kat_matches_survey_probe():
+    st = abi.CurandState()
+    po.lib().orc_curand_init(1984, C.byref(st))
+    got = [po.lib().orc_curand_uniform(C.byref(st)) for _ in range(3)]
+    assert got == pytest.approx([0.195986241, 0.454007715, 0.358994216], abs=5e-10)
+
+
+def test_c1_matches_survey_probe():
+    """BASELINE config 1 through the reference grid: px(200,112)=0xff7f5f3c, px(0,0)=0xff00c0a4, row 224
+    unwritten, 868,442 rays, 4.0 box tests/ray."""
+    cfg = scenes.CONFIGS["c1"]
+    sc = scenes.builtin(cfg.scene)
+    st = po.init_states(cfg.width, cfg.height, full=False)
+    pos, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                            faithful_grid=True, rius_order=1)
+    assert pos[112, 200] == 0xFF7F5F3C
+    assert pos[0, 0] == 0xFF00C0A4
+    assert not pos[224].any() and pos[224, 399] == 0
+    assert cnt.rays == 868442
+    assert cnt.box_tests / cnt.rays == pytest.approx(4.0, abs=0.01)
+    # the survey's checksum (definition not recorded) is 26,494,510; Σ RGB here is within 1 of it
+    s = int(pos.view(np.uint8).reshape(-1, 4)[:, :3].sum())
+    assert abs(s - 26494510) <= 1
+
+
+def test_c1_left_to_right_order_differs_from_probe():
+    """The probe's g++ build filled Random()'s Vec3 right to left; left to right gives another image."""
+    cfg = scenes.CONFIGS["c1"]
+    sc = scenes.builtin(cfg.scene)
+    st = po.init_states(cfg.width, cfg.height, full=False)
+    pos, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                            faithful_grid=True, rius_order=0)
+    assert pos[112, 200] != 0xFF7F5F3C and cnt.rays != 868442
+
+
+# ---------------------------------------------------------------------------------------------------
+# Golden fixtures (regression of the restatement; tests/golden/make_golden.py)
+# ---------------------------------------------------------------------------------------------------
+def test_xorwow_golden():
+    with open(os.path.join(GOLDEN, "xorwow_kat.json")) as f:
+        kat = json.load(f)
+    for seed, v in kat.items():
+        st = abi.CurandState()
+        po.lib().orc_curand_init(int(seed), C.byref(st))
+        assert [st.d] + list(st.v) == v["init"]
+        assert [po.lib().orc_curand(C.byref(st)) for _ in range(8)] == v["raw"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c.name)
+def test_oracle_matches_golden(case):
+    g = load_golden(case.name)
+    cfg = case.cfg()
+    sc = scenes.builtin(cfg.scene)
+    inp = abi.InputStruct.from_buffer_copy(g["inputs"].tobytes())
+    assert bytes(inp) == bytes(cfg.inputs())
+    st = po.init_states(cfg.width, cfg.height, full=not case.faithful_grid)
+    assert digest(st[:, :6]) == g["state_before_sha256"].tobytes()
+    pos, rad, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st,
+                              faithful_grid=case.faithful_grid, rius_order=case.rius_order, radiance=True)
+    np.testing.assert_array_equal(pos, g["pos"])
+    assert digest(st[:, :6]) == g["state_after_sha256"].tobytes()
+    assert digest(rad) == g["radiance_sha256"].tobytes()
+    assert [cnt.rays, cnt.box_tests, cnt.prim_tests, cnt.primary] == [int(x) for x in g["counters"]]
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c.spp <= 8 or c.width <= 128], ids=lambda c: c.name)
+def test_reference_bvh_culling_equals_exact_closest_hit(case):
+    """The reference BVH + AABB culling returns the geometric closest hit on every golden case."""
+    cfg = case.cfg()
+    sc = scenes.builtin(cfg.scene)
+    out = []
+    for exact in (False, True):
+        st = po.init_states(cfg.width, cfg.height)
+        pos, _, cnt = po.render(po.OracleScene(sc, exact=exact), cfg.width, cfg.height, cfg.spp, cfg.depth,
+                                cfg.inputs(), st, rius_order=case.rius_order)
+        out.append((pos, cnt.rays))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+
+
+def test_row_sampling_matches_full_frame():
+    cfg = scenes.CONFIGS["c2"].scaled(64, 40, 2)
+    sc = po.OracleScene(scenes.builtin(cfg.scene))
+    st_full = po.init_states(cfg.width, cfg.height)
+    full, _, _ = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st_full)
+    st = po.init_states(cfg.width, cfg.height)
+    part, _, cnt = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st, rows=(3, 40), row_step=5)
+    rows = list(range(3, 40, 5))
+    np.testing.assert_array_equal(part[rows], full[rows])
+    assert cnt.primary == len(rows) * cfg.width * cfg.spp
+
+
+# ---------------------------------------------------------------------------------------------------
+# Known-answer tests of the restated functions
+# ---------------------------------------------------------------------------------------------------
+def _hit(h, o, d, tmin=0.001, tmax=3.4e38):
+    out = po.Hit()
+    F3 = C.c_float * 3
+    po.lib().orc_hittable_hit(C.byref(h), F3(*o), F3(*d), tmin, tmax, C.byref(out))
+    return out
+
+
+def _sphere(c, r):
+    h = abi.HittableDesc()
+    h.type, h.is_active, h.radius = abi.RT_SPHERE, 1, r
+    h.center[:] = c
+    return h
+
+
+def _rect(t, c, w, hh):
+    h = abi.HittableDesc()
+    h.type, h.is_active, h.width, h.height = t, 1, w, hh
+    h.center[:] = c
+    return h
+
+
+def test_sphere_hit_near_and_far_root():
+    s = _sphere((0.0, 0.0, -5.0), 1.0)
+    h = _hit(s, (0, 0, 0), (0, 0, -1))
+    assert h.hit and h.t == pytest.approx(4.0) and list(h.normal) == pytest.approx([0, 0, 1])
+    # GetSphereUV of the normal (0,0,1): u = (atan2(-1, 0) + π)/2π = 0.25, v = acos(0)/π = 0.5
+    assert h.u == pytest.approx(0.25, abs=1e-6) and h.v == pytest.approx(0.5, abs=1e-6)
+    inside = _hit(s, (0, 0, -5), (0, 0, -1))  # origin inside: near root < tmin → far root
+    assert inside.hit and inside.t == pytest.approx(1.0)
+    assert list(inside.normal) == pytest.approx([0, 0, -1])  # outward, NOT face-flipped (Hittable.cuh:93)
+    assert not _hit(s, (0, 0, 0), (0, 1, 0)).hit
+    assert not _hit(s, (0, 0, 0), (0, 0, -1), tmax=4.0).hit  # strict t < t_max
+    assert not _hit(s, (0, 0, 0), (0, 0, -1), tmin=6.0).hit  # both roots <= t_min
+
+
+def test_rect_hits_and_face_normals():
+    xy = _rect(abi.RT_XYRECT, (0.0, 0.0, -2.0), 2.0, 4.0)
+    h = _hit(xy, (0.5, 1.0, 0.0), (0, 0, -1))
+    assert h.hit and h.t == pytest.approx(2.0)
+    assert (h.u, h.v) == pytest.approx((0.75, 0.75))
+    assert list(h.normal) == pytest.approx([0, 0, 1]) and h.front_face == 1
+    back = _hit(xy, (0.5, 1.0, -4.0), (0, 0, 1))
+    assert back.hit and list(back.normal) == pytest.approx([0, 0, -1]) and back.front_face == 0
+    assert not _hit(xy, (1.5, 0.0, 0.0), (0, 0, -1)).hit  # outside x extent
+    xz = _rect(abi.RT_XZRECT, (0.0, -0.5, 0.0), 1000.0, 1000.0)
+    g = _hit(xz, (0.0, 2.0, 12.0), (0.0, -1.0, 0.0))
+    assert g.hit and g.t == pytest.approx(2.5) and list(g.normal) == pytest.approx([0, 1, 0])
+    # YZ: width spans z, height spans y (Hittable.cuh:255-258)
+    yz = _rect(abi.RT_YZRECT, (3.0, 0.0, 0.0), 10.0, 2.0)
+    assert _hit(yz, (0.0, 0.0, 4.0), (1, 0, 0)).hit
+    assert not _hit(yz, (0.0, 4.0, 0.0), (1, 0, 0)).hit
+    # rect acceptance is inclusive in t (t > t_max rejects, t == t_max accepts)
+    assert _hit(xy, (0.0, 0.0, 0.0), (0, 0, -1), tmax=2.0).hit
+
+
+def _scatter(mat, o, d, hit, seed=1984, order=1):
+    st = abi.CurandState()
+    po.lib().orc_curand_init(seed, C.byref(st))
+    F3 = C.c_float * 3
+    so, sd, att = F3(), F3(), F3()
+    draws = C.c_int(0)
+    ok = po.lib().orc_scatter(C.byref(mat), F3(*o), F3(*d), C.byref(hit), C.byref(st), so, sd, att,
+                              C.byref(draws), order)
+    return ok, list(so), list(sd), list(att), draws.value, st
+
+
+def _mat(t, color=(0.5, 0.5, 0.5), fuzz=0.0, ir=1.5):
+    m = abi.MaterialDesc()
+    m.type, m.fuzz, m.ir = t, fuzz, ir
+    m.albedo.type = abi.RT_CONSTANT
+    m.albedo.color[:] = color
+    return m
+
+
+def _uniforms(seed, n):
+    st = abi.CurandState()
+    po.lib().orc_curand_init(seed, C.byref(st))
+    return [po.lib().orc_curand_uniform(C.byref(st)) for _ in range(n)]
+
+
+def test_lambertian_scatter_direction_and_draws():
+    hit = po.Hit(1, 2.0, (C.c_float * 3)(0.25, -0.5, 1.0), (C.c_float * 3)(0.0, 1.0, 0.0), 0.0, 0.0, 1)
+    ok, so, sd, att, draws, _ = _scatter(_mat(abi.RT_LAMBERTIAN, (0.1, 0.2, 0.3)), (0, 1, 0), (0, -1, 0), hit)
+    assert ok == 1 and att == pytest.approx([0.1, 0.2, 0.3]) and draws % 3 == 0 and draws >= 3
+    # reproduce RandomInUnitSphere's accepted sample (right-to-left fill) and ((p + n) + q) - p
+    u = _uniforms(1984, draws)
+    a, b, c = u[-3:]
+    q = [np.float32(2.0) * np.float32(c) - np.float32(1.0), np.float32(2.0) * np.float32(b) - np.float32(1.0),
+         np.float32(2.0) * np.float32(a) - np.float32(1.0)]
+    p, n = np.float32([0.25, -0.5, 1.0]), np.float32([0.0, 1.0, 0.0])
+    want = ((p + n) + np.float32(q)) - p
+    assert sd == [float(x) for x in want]
+    assert so == [0.25, -0.5, 1.0]
+
+
+def test_metal_scatter_absorbs_below_surface_and_always_draws():
+    hit = po.Hit(1, 1.0, (C.c_float * 3)(0, 0, 0), (C.c_float * 3)(0, 1, 0), 0, 0, 1)
+    ok, _, sd, att, draws, _ = _scatter(_mat(abi.RT_METAL, (0.9, 0.8, 0.7), fuzz=0.0), (0, 1, 0), (1, -1, 0), hit)
+    assert ok == 1 and draws >= 3  # RNG drawn even with fuzz 0 (Material.cuh:79)
+    assert sd == pytest.approx([1 / math.sqrt(2), 1 / math.sqrt(2), 0], abs=1e-6)
+    ok2, _, sd2, _, _, _ = _scatter(_mat(abi.RT_METAL, fuzz=1.0), (0, 1, 0), (1, -1e-4, 0), hit, seed=7)
+    assert ok2 == (1 if sd2[1] > 0 else 0)
+
+
+def test_dielectric_total_internal_reflection_and_one_draw():
+    # exiting ray at a grazing angle: sin θ_t = 1.5·sin θ_i > 1 → reflect with probability 1
+    hit = po.Hit(1, 1.0, (C.c_float * 3)(0, 0, 0), (C.c_float * 3)(0, 1, 0), 0, 0, 1)
+    ok, _, sd, att, draws, _ = _scatter(_mat(abi.RT_DIELECTRIC), (0, -1, 0), (1.0, 0.2, 0.0), hit)
+    assert ok == 1 and att == [1.0, 1.0, 1.0] and draws == 1
+    assert sd == pytest.approx([1.0, -0.2, 0.0])  # un-normalized Reflect(d, n)
+    # normal incidence from outside: Schlick r0 = 0.04 → refract unless ξ < 0.04
+    ok, _, sd, _, draws, _ = _scatter(_mat(abi.RT_DIELECTRIC), (0, 1, 0), (0.0, -1.0, 0.0), hit)
+    xi = _uniforms(1984, 1)[0]
+    assert draws == 1
+    assert sd == pytest.approx([0.0, 1.0, 0.0] if xi < 0.04 else [0.0, -1.0, 0.0])
+
+
+def test_rgb_to_int_clamps_truncates_and_nan():
+    f = po.lib().orc_rgb_to_int
+    assert f(0.0, 0.0, 0.0) == 0xFF000000
+    assert f(255.9, 300.0, -5.0) == 0xFF00FFFF
+    assert f(12.99, 1.5, 128.0) == 0xFF80010C
+    assert f(float("nan"), 3.0, 0.0) == 0xFF000300
