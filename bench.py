@@ -51,7 +51,7 @@ def cpu_baseline(cfg: scenes.Config, target_s: float) -> dict:
                               row_step=step, threads=threads)
         return cnt.rays, time.perf_counter() - t0
 
-    rays, dt = run(cfg.height // 8)  # calibration: 8 rows
+    rays, dt = run(max(1, cfg.height // (4 * threads)))  # calibration: 4 rows per thread
     rate = rays / max(dt, 1e-6)
     step = max(1, int(math.ceil(cfg.height * cfg.width * cfg.spp * 3.1 / max(rate * target_s, 1.0))))
     step = min(step, cfg.height)

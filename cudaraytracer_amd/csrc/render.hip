@@ -120,7 +120,6 @@ struct KParams {
 
 constexpr int kStackMax = 64;
 constexpr int kBlock = 256;
-constexpr int kLdsStackDepth = 24;
 
 enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_HYBRID = 2 };
 
@@ -317,8 +316,8 @@ __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t local_
 }
 
 // Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop.
-template <bool SCENE_LDS, int STACK, bool COUNT_TESTS>
-__global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
+template <bool SCENE_LDS, int STACK, bool COUNT_TESTS, int WAVES_PER_SIMD>
+__global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KParams P) {
     extern __shared__ float4 lds[];
     const float4* nodes = P.nodes;
     const float4* prims = P.prims;
@@ -588,20 +587,36 @@ int hip_check(hipError_t e, const char* what, int code = RT_ERR_DEVICE) {
 
 using KernelFn = void (*)(const dev::KParams);
 
-template <bool L, int S>
+struct Variant {
+    bool scene_lds;
+    int stack;
+    int waves;      // __launch_bounds__ minimum waves per SIMD (1 = compiler's choice)
+    int lds_depth;  // LDS stack entries per lane
+};
+
+// rt_set_variant(i) selects kVariants[i]
+constexpr Variant kVariants[] = {
+    {false, dev::STACK_SCRATCH, 1, 0}, {false, dev::STACK_LDS, 1, 24}, {false, dev::STACK_HYBRID, 1, 0},
+    {true, dev::STACK_SCRATCH, 1, 0},  {true, dev::STACK_LDS, 1, 24},  {true, dev::STACK_HYBRID, 1, 0},
+    {false, dev::STACK_LDS, 6, 20},    {false, dev::STACK_LDS, 8, 16},
+};
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+
+template <bool L, int S, int W>
 KernelFn pick_count(bool count) {
-    return count ? dev::render_kernel<L, S, true> : dev::render_kernel<L, S, false>;
+    return count ? dev::render_kernel<L, S, true, W> : dev::render_kernel<L, S, false, W>;
 }
 
-// variant = scene_lds * 3 + stack_kind
 KernelFn pick(int variant, bool count) {
     switch (variant) {
-    case 0: return pick_count<false, dev::STACK_SCRATCH>(count);
-    case 1: return pick_count<false, dev::STACK_LDS>(count);
-    case 2: return pick_count<false, dev::STACK_HYBRID>(count);
-    case 3: return pick_count<true, dev::STACK_SCRATCH>(count);
-    case 4: return pick_count<true, dev::STACK_LDS>(count);
-    default: return pick_count<true, dev::STACK_HYBRID>(count);
+    case 0: return pick_count<false, dev::STACK_SCRATCH, 1>(count);
+    case 1: return pick_count<false, dev::STACK_LDS, 1>(count);
+    case 2: return pick_count<false, dev::STACK_HYBRID, 1>(count);
+    case 3: return pick_count<true, dev::STACK_SCRATCH, 1>(count);
+    case 4: return pick_count<true, dev::STACK_LDS, 1>(count);
+    case 5: return pick_count<true, dev::STACK_HYBRID, 1>(count);
+    case 6: return pick_count<false, dev::STACK_LDS, 6>(count);
+    default: return pick_count<false, dev::STACK_LDS, 8>(count);
     }
 }
 
@@ -632,6 +647,7 @@ int rt_set_variant(int variant) {
 
 int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) {
     if (!scene || !a) { set_error("rt_render: NULL scene or args"); return RT_ERR_INVALID_ARGUMENT; }
+    if (a->tiling.local_rows == 0 || a->width == 0 || a->height == 0) return RT_OK;  // nothing to render
     if (!a->state) { set_error("rt_render: state is NULL"); return RT_ERR_INVALID_ARGUMENT; }
     if (!a->pos && !a->radiance && !a->accum) { set_error("rt_render: no output buffer"); return RT_ERR_INVALID_ARGUMENT; }
     if ((a->flags & RT_FLAG_ACCUMULATE) && !a->accum) { set_error("rt_render: ACCUMULATE without accum"); return RT_ERR_INVALID_ARGUMENT; }
@@ -719,15 +735,16 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
     const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
     int variant = g_variant;
-    if (variant < 0) variant = scene_lds <= 48 * 1024 ? 3 : 0;  // auto: scene in LDS when it fits
-    const bool v_lds = variant >= 3;
-    const int v_stack = variant % 3;
-    if (v_stack == dev::STACK_LDS && S.depth > (uint32_t)dev::kLdsStackDepth + 1) {
-        set_error("rt_render: BVH too deep for the LDS stack variant");
+    if (variant < 0 || variant >= kNumVariants)  // auto: fastest measured (profiles/r01_*) that fits the BVH
+        variant = S.depth <= (uint32_t)kVariants[6].lds_depth + 1 ? 6 : 0;
+    const Variant& V = kVariants[variant];
+    // near-first traversal holds at most one deferred child per level below the root
+    if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
+        set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
     }
-    size_t lds_bytes = (v_lds ? scene_lds : 0) +
-                       (v_stack == dev::STACK_LDS ? (size_t)dev::kLdsStackDepth * dev::kBlock * 4 : 0);
+    size_t lds_bytes = (V.scene_lds ? scene_lds : 0) +
+                       (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * dev::kBlock * 4 : 0);
     if (lds_bytes > kLdsLimit) {
         set_error("rt_render: scene does not fit in LDS for this variant");
         return RT_ERR_UNSUPPORTED;
@@ -761,7 +778,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
 
 int rt_render_init(rt_curand_state* d_state, uint32_t width, uint32_t height, const rt_tiling* tiling,
                    uint64_t seed_base, rt_stream stream) {
-    if (!d_state || !tiling) { set_error("rt_render_init: NULL argument"); return RT_ERR_INVALID_ARGUMENT; }
+    if (!tiling) { set_error("rt_render_init: NULL tiling"); return RT_ERR_INVALID_ARGUMENT; }
+    if ((size_t)width * tiling->local_rows == 0) return RT_OK;  // nothing to seed
+    if (!d_state) { set_error("rt_render_init: NULL state"); return RT_ERR_INVALID_ARGUMENT; }
     if (tiling->band_rows == 0 || tiling->num_ranks == 0 || tiling->rank >= tiling->num_ranks) {
         set_error("rt_render_init: invalid tiling");
         return RT_ERR_INVALID_ARGUMENT;

@@ -23,7 +23,7 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 3, 4, 5]
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7]
 
 
 @pytest.fixture(autouse=True)
@@ -266,6 +266,7 @@ def test_invalid_arguments_fail_loudly():
         r.render(ds, 1, 1, cfg.inputs())
     a = abi.RenderArgs()
     a.pos, a.width, a.height = r.pos.data_ptr(), 32, 16
+    a.tiling = abi.Tiling(16, 1, 0, 16)
     assert lib().rt_render(ds.handle, C.byref(a), None) == -1  # NULL state
     assert b"state" in lib().rt_last_error()
 
