@@ -29,6 +29,7 @@ EXPORTED = [
     "rt_set_timing",
     "rt_last_kernel_ms",
     "rt_set_variant",
+    "rt_set_tuning",
     "rt_glibc_srand",
     "rt_glibc_rand_next",
     "rt_builtin_scene",
@@ -60,6 +61,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_set_timing.argtypes = [C.c_int]
     lib.rt_last_kernel_ms.restype = C.c_float
     lib.rt_set_variant.argtypes = [C.c_int]
+    lib.rt_set_tuning.argtypes = [C.c_int, C.c_int]
     lib.rt_glibc_srand.argtypes = [P(abi.GlibcRand), C.c_uint32]
     lib.rt_glibc_rand_next.argtypes = [P(abi.GlibcRand)]
     lib.rt_glibc_rand_next.restype = C.c_int32

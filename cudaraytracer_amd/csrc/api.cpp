@@ -65,6 +65,7 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     d.num_mats = h.num_mats;
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
+    d.has_textures = h.has_textures;
     d.device_bytes = (h.nodes.size() + h.prims.size() + h.mats.size()) * 4 + h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;
@@ -242,6 +243,10 @@ int rt_scene_update_materials(rt_scene* scene, const rt_material_desc* materials
     if (rc) { set_error("rt_scene_update_materials: " + err); return rc; }
     for (uint32_t i = 0; i < num_materials; i++)
         if (materials[i].type != RT_DIELECTRIC && materials[i].albedo.type == RT_IMAGE) scene->dev.has_image_textures = true;
+    bool tex = false;
+    for (uint32_t i = 0; i < num_materials; i++)
+        if (materials[i].type != RT_DIELECTRIC && materials[i].albedo.type != RT_CONSTANT) tex = true;
+    scene->dev.has_textures = tex;
     if (!packed.empty()) {
         hipError_t e = hipMemcpy((void*)scene->dev.mats, packed.data(), packed.size() * 4, hipMemcpyHostToDevice);
         if (e != hipSuccess) return hip_fail(e, "rt_scene_update_materials: hipMemcpy");

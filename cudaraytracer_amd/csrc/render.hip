@@ -116,12 +116,13 @@ struct KParams {
     float fov_fwd[3];  // inputs.fov * forwardV           (Kernel.cu:142)
     float k10_fwd[3];  // (1.0f / inputs.fov * 10.0f) * forwardV (Kernel.cu:143)
     float bg0[3], bg1[3];
+    uint32_t regen_threshold;  // v2: lanes still tracing below which finished lanes are regenerated
 };
 
 constexpr int kStackMax = 64;
 constexpr int kBlock = 256;
 
-enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_HYBRID = 2 };
+enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_HYBRID = 2, STACK_LDS16 = 3 };
 
 // Per-lane traversal stacks -------------------------------------------------------------------------
 struct ScratchStack {
@@ -169,7 +170,13 @@ template <> struct StackOf<STACK_HYBRID> { using T = HybridStack; };
 
 struct Counts {
     uint32_t rays, boxes, prims, primary;
+    uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
 };
+
+// 1 on the lowest active lane of the wave, 0 elsewhere (diagnostic wave-iteration counts).
+__device__ __forceinline__ uint32_t wave_leader() {
+    return __lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1) ? 1u : 0u;
+}
 
 constexpr int kEmpty = (int)0x80000000;
 constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX, rec) (Kernel.cu:40)
@@ -210,7 +217,10 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
             const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
             const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
             const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
-            if (COUNT) cnt.boxes += 2;
+            if (COUNT) {
+                cnt.boxes += 2;
+                cnt.wnode += wave_leader();
+            }
             const bool h0 = c0min <= c0max;
             const bool h1 = c1min <= c1max;
             const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
@@ -227,12 +237,15 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
         if (node == kEmpty) break;
         // leaf: primitives [first, first + count)
         const uint32_t leaf = ~(uint32_t)node;
-        const uint32_t first = leaf >> 4, count = leaf & 15u;
+        const uint32_t first = leaf >> 2, count = (leaf & 3u) + 1u;
         for (uint32_t i = first; i < first + count; i++) {
             const float4 p0 = prims[2 * i + 0];
             const float4 p1 = prims[2 * i + 1];
             const uint32_t type = __float_as_uint(p1.w) & 15u;
-            if (COUNT) cnt.prims++;
+            if (COUNT) {
+                cnt.prims++;
+                cnt.wleaf += wave_leader();
+            }
             if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
                 const f3 oc = sub(o, xyz(p0));
                 const float b = dot(oc, d);
@@ -315,194 +328,145 @@ __device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t local_
     return (band * P.num_ranks + P.rank) * P.band_rows + within;
 }
 
-// Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop.
-template <bool SCENE_LDS, int STACK, bool COUNT_TESTS, int WAVES_PER_SIMD>
-__global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KParams P) {
-    extern __shared__ float4 lds[];
-    const float4* nodes = P.nodes;
-    const float4* prims = P.prims;
-    uint32_t* lds_stack = nullptr;
-    if constexpr (SCENE_LDS) {
-        const uint32_t nn = P.num_nodes * 4, np = P.num_prims * 2;
-        for (uint32_t i = threadIdx.x; i < nn; i += kBlock) lds[i] = P.nodes[i];
-        for (uint32_t i = threadIdx.x; i < np; i += kBlock) lds[nn + i] = P.prims[i];
-        __syncthreads();
-        nodes = lds;
-        prims = lds + nn;
-        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)(lds + nn + np);
-    } else {
-        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)lds;
+// Launch-uniform camera / background terms (kernel arguments, SGPR-resident).
+struct Camera {
+    f3 origin, up, right, fov_fwd, k10_fwd;
+    float xf, yf;  // (x - center.x()), (center.y() - y) of this lane's pixel (Kernel.cu:139-140)
+};
+
+// Camera ray of one sample (Kernel.cu:139-146): two uniforms, then the reference's plane construction.
+template <class PP>
+__device__ __forceinline__ void camera_ray(PP P, const Camera& cam, Rng& rng, f3& ro, f3& rd) {
+    const float u = (cam.xf + uniform(rng)) / P->width_f;
+    const float v = (cam.yf + uniform(rng)) / P->width_f;
+    const f3 dist = add(scale(u, cam.right), scale(v, cam.up));
+    const f3 start = add(add(scale(P->near_plane, dist), cam.origin), cam.fov_fwd);
+    const f3 second = add(add(scale(P->far_plane, dist), cam.k10_fwd), cam.origin);
+    ro = start;
+    rd = normalize(sub(second, start));
+}
+
+// One iteration of color()'s bounce loop after the closest-hit query (Kernel.cu:40-76): sky on a miss,
+// emission, or Scatter of the hit material.  Returns true when the path ended (contribution in `contrib`,
+// `emitted * cur_attenuation` or `cur_attenuation * sky`); false when it continues with (ro, rd, att).
+template <bool TEX = true, class PP>
+__device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, int hit, float t, f3& ro,
+                                      f3& rd, f3& att, Rng& rng, bool rtl, f3& contrib) {
+    if (hit < 0) {  // sky (Kernel.cu:41-44)
+        const f3 unit_direction = unit_vector(rd);
+        const float tt = 0.5f * (unit_direction.y + 1.0f);
+        const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
+        contrib = mulv(att, c);
+        return true;
     }
-
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t bx = blockIdx.x % P.tiles_x, by = blockIdx.x / P.tiles_x;
-    const uint32_t x = bx * 16 + (wave & 1u) * 8 + (lane & 7u);
-    const uint32_t ly = by * 16 + (wave >> 1) * 8 + (lane >> 3);
-    if (x >= P.width || ly >= P.local_rows) return;
-    const uint32_t g = global_row(P, ly);
-    if (x >= P.grid_w || g >= P.grid_h) return;  // faithful floor-division grid (Kernel.cu:184)
-    const size_t pix = (size_t)ly * P.width + x;
-
-    uint32_t* st = P.state + pix * 12;
-    const uint4 s03 = *reinterpret_cast<const uint4*>(st);
-    const uint2 s45 = *reinterpret_cast<const uint2*>(st + 4);
-    Rng rng{s03.x, s03.y, s03.z, s03.w, s45.x, s45.y};
-
-    const f3 origin = mk(P.origin[0], P.origin[1], P.origin[2]);
-    const f3 up = mk(P.up[0], P.up[1], P.up[2]);
-    const f3 right = mk(P.right[0], P.right[1], P.right[2]);
-    const f3 fov_fwd = mk(P.fov_fwd[0], P.fov_fwd[1], P.fov_fwd[2]);
-    const f3 k10_fwd = mk(P.k10_fwd[0], P.k10_fwd[1], P.k10_fwd[2]);
-    const f3 bg0 = mk(P.bg0[0], P.bg0[1], P.bg0[2]);
-    const f3 bg1 = mk(P.bg1[0], P.bg1[1], P.bg1[2]);
-    const bool rtl = P.rius_rtl != 0;
-    const float xf = (float)(int)x - P.cx;       // (x - center.x())     (Kernel.cu:139)
-    const float yf = P.cy - (float)(int)g;       // (center.y() - y)     (Kernel.cu:140)
-
-    Counts cnt{0, 0, 0, 0};
-    f3 col = mk(0.0f, 0.0f, 0.0f);
-    f3 att = mk(1.0f, 1.0f, 1.0f);
-    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
-    uint32_t sample = 0, depth = 0;
-    bool need_camera = true;
-
-    if (P.spp > 0) {
-        while (true) {
-            if (need_camera) {  // camera ray (Kernel.cu:139-146)
-                const float u = (xf + uniform(rng)) / P.width_f;
-                const float v = (yf + uniform(rng)) / P.width_f;
-                const f3 dist = add(scale(u, right), scale(v, up));
-                const f3 start = add(add(scale(P.near_plane, dist), origin), fov_fwd);
-                const f3 second = add(add(scale(P.far_plane, dist), k10_fwd), origin);
-                ro = start;
-                rd = normalize(sub(second, start));
-                att = mk(1.0f, 1.0f, 1.0f);
-                depth = 0;
-                need_camera = false;
-                cnt.primary++;
-            }
-            f3 contrib;
-            bool done = true;
-            if (depth >= P.max_depth) {
-                contrib = mk(0.0f, 0.0f, 0.0f);  // exceeded recursion (Kernel.cu:79)
-            } else {
-                cnt.rays++;
-                const float a_dd = dot(rd, rd);
-                float t;
-                const int hit = trace<STACK, COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, lds_stack, cnt);
-                if (hit < 0) {  // sky (Kernel.cu:41-44)
-                    const f3 unit_direction = unit_vector(rd);
-                    const float tt = 0.5f * (unit_direction.y + 1.0f);
-                    const f3 c = add(scale(1.0f - tt, bg0), scale(tt, bg1));
-                    contrib = mulv(att, c);
-                } else {
-                    const float4 p0 = prims[2 * hit + 0];
-                    const float4 p1 = prims[2 * hit + 1];
-                    const uint32_t tag = __float_as_uint(p1.w);
-                    const uint32_t type = tag & 15u, mat = tag >> 4;
-                    const float4 m0 = P.mats[3 * mat + 0];
-                    const uint32_t mbits = __float_as_uint(m0.x);
-                    const uint32_t mtype = mbits & 15u, ttype = (mbits >> 4) & 15u;
-                    f3 p, normal;
-                    float hu = 0.0f, hv = 0.0f;
-                    if (type == RT_SPHERE) {
-                        p = add(ro, scale(t, rd));
-                        normal = divs(sub(p, xyz(p0)), p0.w);
-                        if (ttype == RT_IMAGE && mtype != RT_DIELECTRIC) {  // GetSphereUV (Hittable.cuh:119-125)
-                            const float theta = acosf(-normal.y);
-                            const float phi = atan2f(-normal.z, normal.x) + 3.141592654f;
-                            hu = phi / (2 * 3.141592654f);
-                            hv = theta / 3.141592654f;
-                        }
-                    } else {
-                        const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
-                        const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
-                        const float xx = oa + t * da;
-                        const float yy = ob + t * db;
-                        hu = (xx - p0.y) / (p0.z - p0.y);
-                        hv = (yy - p0.w) / (p1.x - p0.w);
-                        const f3 outward = type == RT_XYRECT ? mk(0.0f, 0.0f, 1.0f)
-                                           : type == RT_XZRECT ? mk(0.0f, 1.0f, 0.0f)
-                                                               : mk(1.0f, 0.0f, 0.0f);
-                        const bool front = dot(rd, outward) < 0;  // SetFaceNormal (Hittable.cuh:23-27)
-                        normal = front ? outward : neg(outward);
-                        p = add(ro, scale(t, rd));
-                    }
-                    if (mtype == RT_DIFFUSELIGHT) {  // DiffuseLight::Emitted (Material.cuh:164-176)
-                        const float4 m1 = P.mats[3 * mat + 1], m2 = P.mats[3 * mat + 2];
-                        const f3 e = scale(m0.z, texture_value(m0, m1, m2, ttype, hu, hv, p, P.imgs, P.texels));
-                        contrib = mulv(e, att);
-                    } else if (mtype == RT_DIELECTRIC) {  // Dielectric::Scatter (Material.cuh:106-136)
-                        const float ir = m0.y;
-                        const f3 reflected = reflect(rd, normal);
-                        f3 outward_normal;
-                        float ni_over_nt, cosine;
-                        if (dot(rd, normal) > 0.0f) {
-                            outward_normal = neg(normal);
-                            ni_over_nt = ir;
-                            cosine = dot(rd, normal) / length(rd);
-                            cosine = sqrtf(1.0f - ir * ir * (1 - cosine * cosine));
-                        } else {
-                            outward_normal = normal;
-                            ni_over_nt = 1.0f / ir;
-                            cosine = -dot(rd, normal) / length(rd);
-                        }
-                        // Refract (Math.cuh:292-304)
-                        const f3 uv = unit_vector(rd);
-                        const float dt = dot(uv, outward_normal);
-                        const float discriminant = 1.0f - ni_over_nt * ni_over_nt * (1 - dt * dt);
-                        f3 refracted = mk(0.0f, 0.0f, 0.0f);
-                        float reflect_prob = 1.0f;
-                        if (discriminant > 0) {
-                            refracted = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))),
-                                            scale(sqrtf(discriminant), outward_normal));
-                            float r0 = (1.0f - ir) / (1.0f + ir);  // Reflectance (Material.cuh:139-145)
-                            r0 = r0 * r0;
-                            const float xs = 1.0f - cosine;
-                            const float x2 = xs * xs;
-                            reflect_prob = r0 + (1.0f - r0) * ((x2 * x2) * xs);
-                        }
-                        ro = p;
-                        rd = uniform(rng) < reflect_prob ? reflected : refracted;
-                        done = false;
-                    } else {
-                        const f3 q = random_in_unit_sphere(rng, rtl);
-                        const float4 m1 = P.mats[3 * mat + 1];
-                        f3 attenuation;
-                        bool ok = true;
-                        if (mtype == RT_LAMBERTIAN) {  // Lambertian::Scatter (Material.cuh:43-62)
-                            const f3 target = add(add(p, normal), q);
-                            rd = sub(target, p);
-                        } else {  // Metal::Scatter (Material.cuh:75-94)
-                            const f3 reflected = reflect(unit_vector(rd), normal);
-                            rd = add(reflected, scale(m0.y, q));
-                            ok = dot(rd, normal) > 0;
-                        }
-                        if (ttype == RT_CONSTANT) {
-                            attenuation = xyz(m1);
-                        } else {
-                            const float4 m2 = P.mats[3 * mat + 2];
-                            attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, P.imgs, P.texels);
-                        }
-                        ro = p;
-                        if (ok) {
-                            att = mulv(attenuation, att);
-                            done = false;
-                        } else {
-                            contrib = mulv(mk(0.0f, 0.0f, 0.0f), att);  // emitted * cur_attenuation
-                        }
-                    }
-                    if (!done) depth++;
-                }
-            }
-            if (done) {
-                col = add(col, contrib);
-                if (++sample == P.spp) break;
-                need_camera = true;
-            }
+    const float4 p0 = prims[2 * hit + 0];
+    const float4 p1 = prims[2 * hit + 1];
+    const uint32_t tag = __float_as_uint(p1.w);
+    const uint32_t type = tag & 15u, mat = tag >> 4;
+    const float4 m0 = P->mats[3 * mat + 0];
+    const uint32_t mbits = __float_as_uint(m0.x);
+    const uint32_t mtype = mbits & 15u, ttype = (mbits >> 4) & 15u;
+    f3 p, normal;
+    float hu = 0.0f, hv = 0.0f;
+    if (type == RT_SPHERE) {  // hit record of Sphere::Hit (Hittable.cuh:91-95)
+        p = add(ro, scale(t, rd));
+        normal = divs(sub(p, xyz(p0)), p0.w);
+        if (TEX && ttype == RT_IMAGE && mtype != RT_DIELECTRIC) {  // GetSphereUV (Hittable.cuh:119-125)
+            const float theta = acosf(-normal.y);
+            const float phi = atan2f(-normal.z, normal.x) + 3.141592654f;
+            hu = phi / (2 * 3.141592654f);
+            hv = theta / 3.141592654f;
         }
+    } else {  // hit record of *Rect::Hit (Hittable.cuh:155-166)
+        const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+        const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+        const float xx = oa + t * da;
+        const float yy = ob + t * db;
+        hu = (xx - p0.y) / (p0.z - p0.y);
+        hv = (yy - p0.w) / (p1.x - p0.w);
+        const f3 outward = type == RT_XYRECT ? mk(0.0f, 0.0f, 1.0f)
+                           : type == RT_XZRECT ? mk(0.0f, 1.0f, 0.0f)
+                                               : mk(1.0f, 0.0f, 0.0f);
+        const bool front = dot(rd, outward) < 0;  // SetFaceNormal (Hittable.cuh:23-27)
+        normal = front ? outward : neg(outward);
+        p = add(ro, scale(t, rd));
     }
+    if (mtype == RT_DIFFUSELIGHT) {  // DiffuseLight::Emitted (Material.cuh:164-176)
+        const float4 m1 = P->mats[3 * mat + 1];
+        f3 tex = xyz(m1);
+        if (TEX && ttype != RT_CONSTANT) {
+            const float4 m2 = P->mats[3 * mat + 2];
+            tex = texture_value(m0, m1, m2, ttype, hu, hv, p, P->imgs, P->texels);
+        }
+        const f3 e = scale(m0.z, tex);
+        contrib = mulv(e, att);
+        return true;
+    }
+    if (mtype == RT_DIELECTRIC) {  // Dielectric::Scatter (Material.cuh:106-136); attenuation (1,1,1)
+        // Evaluated in an order that keeps few values live: every quantity is the same binary32 value the
+        // reference computes (pure functions of rd, normal, ir), and only the chosen direction is formed.
+        const float ir = m0.y;
+        const float dn = dot(rd, normal);
+        const float len = length(rd);
+        const bool exiting = dn > 0.0f;
+        float cosine = (exiting ? dn : -dn) / len;
+        if (exiting) cosine = sqrtf(1.0f - ir * ir * (1 - cosine * cosine));
+        const float ni_over_nt = exiting ? ir : 1.0f / ir;
+        const f3 outward_normal = exiting ? neg(normal) : normal;
+        // Refract (Math.cuh:292-304): uv = UnitVector(v) = v / v.Length()
+        const f3 uv = divs(rd, len);
+        const float dt = dot(uv, outward_normal);
+        const float discriminant = 1.0f - ni_over_nt * ni_over_nt * (1 - dt * dt);
+        float reflect_prob = 1.0f;
+        if (discriminant > 0) {
+            float r0 = (1.0f - ir) / (1.0f + ir);  // Reflectance (Material.cuh:139-145)
+            r0 = r0 * r0;
+            const float xs = 1.0f - cosine;
+            const float x2 = xs * xs;
+            reflect_prob = r0 + (1.0f - r0) * ((x2 * x2) * xs);
+        }
+        const bool refl = uniform(rng) < reflect_prob;
+        if (refl) {
+            rd = reflect(rd, normal);
+        } else if (discriminant > 0) {
+            rd = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))), scale(sqrtf(discriminant), outward_normal));
+        } else {
+            rd = mk(0.0f, 0.0f, 0.0f);  // uninitialised `refracted` in the reference (ξ = 1.0, TIR)
+        }
+        ro = p;
+        return false;
+    }
+    const f3 q = random_in_unit_sphere(rng, rtl);
+    const float4 m1 = P->mats[3 * mat + 1];
+    f3 attenuation;
+    bool ok = true;
+    if (mtype == RT_LAMBERTIAN) {  // Lambertian::Scatter (Material.cuh:43-62)
+        const f3 target = add(add(p, normal), q);
+        rd = sub(target, p);
+    } else {  // Metal::Scatter (Material.cuh:75-94)
+        const f3 reflected = reflect(unit_vector(rd), normal);
+        rd = add(reflected, scale(m0.y, q));
+        ok = dot(rd, normal) > 0;
+    }
+    if (!TEX || ttype == RT_CONSTANT) {
+        attenuation = xyz(m1);
+    } else {
+        const float4 m2 = P->mats[3 * mat + 2];
+        attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, P->imgs, P->texels);
+    }
+    ro = p;
+    if (ok) {
+        att = mulv(attenuation, att);
+        return false;
+    }
+    contrib = mulv(mk(0.0f, 0.0f, 0.0f), att);  // emitted * cur_attenuation
+    return true;
+}
 
+// Pixel epilogue (Kernel.cu:149-157): RNG state store, average, gamma 2, RGBA8 pack; optional outputs.
+template <bool COUNT_TESTS>
+__device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint32_t* st, const Rng& rng, f3 col,
+                                             const Counts& cnt) {
     if (!(P.flags & RT_FLAG_NO_STATE_WRITEBACK)) {
         *reinterpret_cast<uint4*>(st) = make_uint4(rng.d, rng.v0, rng.v1, rng.v2);
         *reinterpret_cast<uint2*>(st + 4) = make_uint2(rng.v3, rng.v4);
@@ -521,15 +485,591 @@ __global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KP
     }
     if (P.radiance) P.radiance[pix] = make_float4(c.x, c.y, c.z, 1.0f);
     if (P.pos) P.pos[pix] = rgb_to_int(255.0f * sqrtf(c.x), 255.0f * sqrtf(c.y), 255.0f * sqrtf(c.z));
-
     if (P.counters) {
         atomicAdd(&P.counters[0], (unsigned long long)cnt.rays);
         if (COUNT_TESTS) {
             atomicAdd(&P.counters[1], (unsigned long long)cnt.boxes);
             atomicAdd(&P.counters[2], (unsigned long long)cnt.prims);
+            atomicAdd(&P.counters[4], (unsigned long long)cnt.wnode);
+            atomicAdd(&P.counters[5], (unsigned long long)cnt.wleaf);
+            atomicAdd(&P.counters[6], (unsigned long long)cnt.wshade);
         }
         atomicAdd(&P.counters[3], (unsigned long long)cnt.primary);
     }
+}
+
+// Lane → pixel.  BLOCK = 256: a workgroup covers a 16×16 tile, each wave an 8×8 sub-tile (P.tiles_x =
+// ceil(W/16)); BLOCK = 64: one wave per workgroup covering an 8×8 tile (P.tiles_x = ceil(W/8)).  Returns
+// false for lanes outside the (local) image or outside the faithful floor-division grid (Kernel.cu:184).
+template <int BLOCK = kBlock>
+__device__ __forceinline__ bool lane_pixel(const KParams& P, uint32_t& x, uint32_t& g, size_t& pix) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t bx = blockIdx.x % P.tiles_x, by = blockIdx.x / P.tiles_x;
+    uint32_t ly;
+    if constexpr (BLOCK == 64) {
+        x = bx * 8 + (lane & 7u);
+        ly = by * 8 + (lane >> 3);
+    } else {
+        x = bx * 16 + (wave & 1u) * 8 + (lane & 7u);
+        ly = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    }
+    if (x >= P.width || ly >= P.local_rows) return false;
+    g = global_row(P, ly);
+    if (x >= P.grid_w || g >= P.grid_h) return false;
+    pix = (size_t)ly * P.width + x;
+    return true;
+}
+
+template <class PP>
+__device__ __forceinline__ Camera lane_camera(PP P, uint32_t x, uint32_t g) {
+    Camera c;
+    c.origin = mk(P->origin[0], P->origin[1], P->origin[2]);
+    c.up = mk(P->up[0], P->up[1], P->up[2]);
+    c.right = mk(P->right[0], P->right[1], P->right[2]);
+    c.fov_fwd = mk(P->fov_fwd[0], P->fov_fwd[1], P->fov_fwd[2]);
+    c.k10_fwd = mk(P->k10_fwd[0], P->k10_fwd[1], P->k10_fwd[2]);
+    c.xf = (float)(int)x - P->cx;
+    c.yf = P->cy - (float)(int)g;
+    return c;
+}
+
+// The kernel-argument block as a constant-address-space pointer the compiler cannot see through: fields
+// read through it are re-loaded with s_load where they are used, instead of being held in registers
+// across the traversal loop (launch-uniform camera/shading constants otherwise overflow the SGPR budget
+// and get parked in VGPRs, costing occupancy).
+typedef __attribute__((address_space(4))) const KParams KParamsC;
+__device__ __forceinline__ KParamsC* kparams_reload() {
+    KParamsC* p = (KParamsC*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+__device__ __forceinline__ Rng load_rng(const uint32_t* st) {
+    const uint4 s03 = *reinterpret_cast<const uint4*>(st);
+    const uint2 s45 = *reinterpret_cast<const uint2*>(st + 4);
+    return Rng{s03.x, s03.y, s03.z, s03.w, s45.x, s45.y};
+}
+
+// Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop: every
+// iteration traces one ray per lane to completion (trace()), then shades it.
+template <bool SCENE_LDS, int STACK, bool COUNT_TESTS, int WAVES_PER_SIMD>
+__global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KParams P) {
+    extern __shared__ float4 lds[];
+    const float4* nodes = P.nodes;
+    const float4* prims = P.prims;
+    uint32_t* lds_stack = nullptr;
+    if constexpr (SCENE_LDS) {
+        const uint32_t nn = P.num_nodes * 4, np = P.num_prims * 2;
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlock) lds[i] = P.nodes[i];
+        for (uint32_t i = threadIdx.x; i < np; i += kBlock) lds[nn + i] = P.prims[i];
+        __syncthreads();
+        nodes = lds;
+        prims = lds + nn;
+        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)(lds + nn + np);
+    } else {
+        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)lds;
+    }
+    uint32_t x, g;
+    size_t pix;
+    if (!lane_pixel(P, x, g, pix)) return;
+    uint32_t* st = P.state + pix * 12;
+    Rng rng = load_rng(st);
+    const Camera cam = lane_camera(&P, x, g);
+    const bool rtl = P.rius_rtl != 0;
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    uint32_t sample = 0, depth = 0;
+    bool need_camera = true;
+
+    if (P.spp > 0) {
+        while (true) {
+            if (need_camera) {
+                camera_ray(&P, cam, rng, ro, rd);
+                att = mk(1.0f, 1.0f, 1.0f);
+                depth = 0;
+                need_camera = false;
+                cnt.primary++;
+            }
+            f3 contrib;
+            bool done = true;
+            if (depth >= P.max_depth) {
+                contrib = mk(0.0f, 0.0f, 0.0f);  // exceeded recursion (Kernel.cu:79)
+            } else {
+                cnt.rays++;
+                const float a_dd = dot(rd, rd);
+                float t;
+                const int hit = trace<STACK, COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, lds_stack, cnt);
+                if (COUNT_TESTS) cnt.wshade += wave_leader();
+                done = shade(&P, prims, hit, t, ro, rd, att, rng, rtl, contrib);
+                if (!done) depth++;
+            }
+            if (done) {
+                col = add(col, contrib);
+                if (++sample == P.spp) break;
+                need_camera = true;
+            }
+        }
+    }
+    finish_pixel<COUNT_TESTS>(P, pix, st, rng, col, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v2: resumable traversal.  Each lane carries its traversal state (node, postponed leaf, LDS stack,
+// closest hit) across iterations of one loop, in the structure of Aila & Laine's persistent
+// "while-while" kernel with speculative traversal:
+//   * internal nodes are visited until every lane of the wave has found a leaf; a lane's first leaf is
+//     postponed and it keeps traversing, so leaf tests run with most lanes active;
+//   * when fewer than `regen_threshold` lanes are still tracing, the wave leaves the traversal loop and
+//     the lanes whose query finished shade their hit and start their next ray (bounce or next sample),
+//     instead of idling until the slowest ray of the wave is done (path regeneration).
+// Per lane the sequence of rays, RNG draws and arithmetic is exactly that of render_kernel.
+// ---------------------------------------------------------------------------------------------------
+constexpr int kSentinel = 0x7fffffff;  // traversal finished (internal node ids are < it, leaves < 0)
+enum LaneMode { MODE_TRAV = 0, MODE_SHADE = 1, MODE_DONE = 2 };
+
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, int BLOCK>
+__global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void render_kernel_v2(const KParams P) {
+    extern __shared__ float4 lds[];
+    uint32_t* const stk = (uint32_t*)lds + threadIdx.x;  // [depth][BLOCK] per-lane stacks
+    const float4* __restrict__ nodes = P.nodes;
+    const float4* __restrict__ prims = P.prims;
+    uint32_t x, g;
+    size_t pix;
+    if (!lane_pixel<BLOCK>(P, x, g, pix)) return;
+    uint32_t* st = P.state + pix * 12;
+    Rng rng = load_rng(st);
+    const Camera cam = lane_camera(&P, x, g);
+    const bool rtl = P.rius_rtl != 0;
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    uint32_t sample = 0, depth = 0;
+    // traversal state of the current ray
+    int node = kSentinel, leaf = 0, hit = -1;
+    uint32_t sp = 0;
+    float t_best = FLT_MAX, a_dd = 0.0f;
+    f3 invd = ro, oi = ro;
+    int mode = MODE_DONE;
+
+    // Start the closest-hit query of (ro, rd) (BVHNode::Hit with t in (0.001, FLT_MAX), Kernel.cu:40).
+    auto start_trace = [&]() {
+        cnt.rays++;
+        a_dd = dot(rd, rd);
+        invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
+                  fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
+                  fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
+        oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
+        t_best = FLT_MAX;
+        hit = -1;
+        node = P.num_nodes ? 0 : kSentinel;
+        leaf = 0;
+        sp = 0;
+        mode = MODE_TRAV;
+    };
+    // A path ended with `contrib`: accumulate (Kernel.cu:147) and begin the next sample, or finish.
+    auto next_sample = [&](f3 contrib) {
+        col = add(col, contrib);
+        while (++sample < P.spp) {
+            camera_ray(&P, cam, rng, ro, rd);
+            att = mk(1.0f, 1.0f, 1.0f);
+            depth = 0;
+            cnt.primary++;
+            if (P.max_depth > 0) {
+                start_trace();
+                return;
+            }
+            col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+        }
+        mode = MODE_DONE;
+    };
+
+    if (P.spp > 0) {
+        sample = (uint32_t)-1;
+        next_sample(mk(0.0f, 0.0f, 0.0f));  // col += 0 leaves col = +0 bit-exactly
+    }
+    const uint32_t threshold = P.regen_threshold;
+
+    while (true) {
+        if (mode == MODE_TRAV) {
+            while (node != kSentinel || leaf < 0) {
+                // internal nodes until every lane here has a postponed leaf.  Branch-free visit: the two
+                // stack entries a visit may pop are read before the node data arrives, the far child is
+                // written unconditionally above the stack top (kept only when both children are hit).
+                while ((uint32_t)node < (uint32_t)kSentinel) {
+                    const int top1 = (int)stk[((sp > 0u ? sp : 1u) - 1u) * BLOCK];
+                    const int top2 = (int)stk[((sp > 1u ? sp : 2u) - 2u) * BLOCK];
+                    const float4 n0 = nodes[4 * node + 0];
+                    const float4 n1 = nodes[4 * node + 1];
+                    const float4 n2 = nodes[4 * node + 2];
+                    const float4 n3 = nodes[4 * node + 3];
+                    const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
+                    const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
+                    const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
+                    const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
+                    const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
+                    const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
+                    const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+                    const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+                    const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+                    const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+                    if (COUNT_TESTS) {
+                        cnt.boxes += 2;
+                        cnt.wnode += wave_leader();
+                    }
+                    const bool h0 = c0min <= c0max;
+                    const bool h1 = c1min <= c1max;
+                    const bool both = h0 && h1, none = !(h0 || h1);
+                    const bool swap = c1min < c0min;
+                    const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+                    const int nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
+                    const int farc = swap ? ch0 : ch1;
+                    stk[sp * BLOCK] = (uint32_t)farc;
+                    int nxt = none ? (sp > 0u ? top1 : kSentinel) : nearc;
+                    uint32_t nsp = both ? sp + 1u : ((none && sp > 0u) ? sp - 1u : sp);
+                    // first leaf: postpone it and pop the next entry (the stack top after this visit)
+                    const bool postpone = nxt < 0 && leaf == 0;
+                    const int after_top = both ? farc : (none ? (sp > 1u ? top2 : kSentinel) : (sp > 0u ? top1 : kSentinel));
+                    leaf = postpone ? nxt : leaf;
+                    nxt = postpone ? after_top : nxt;
+                    nsp = (postpone && nsp > 0u) ? nsp - 1u : nsp;
+                    node = nxt;
+                    sp = nsp;
+                    if (__ballot(leaf == 0) == 0) break;
+                }
+                // postponed leaves
+                while (leaf < 0) {
+                    const uint32_t l = ~(uint32_t)leaf;
+                    const uint32_t first = l >> 2, count = (l & 3u) + 1u;
+                    for (uint32_t i = first; i < first + count; i++) {
+                        const float4 p0 = prims[2 * i + 0];
+                        const float4 p1 = prims[2 * i + 1];
+                        const uint32_t type = __float_as_uint(p1.w) & 15u;
+                        if (COUNT_TESTS) {
+                            cnt.prims++;
+                            cnt.wleaf += wave_leader();
+                        }
+                        if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                            const f3 oc = sub(ro, xyz(p0));
+                            const float b = dot(oc, rd);
+                            const float c = dot(oc, oc) - p1.x;
+                            const float disc = b * b - a_dd * c;
+                            if (disc > 0) {
+                                const float sq = sqrtf(disc);
+                                float t = (-b - sq) / a_dd;
+                                if (t < t_best && t > kTmin) {
+                                    t_best = t;
+                                    hit = (int)i;
+                                } else {
+                                    t = (-b + sq) / a_dd;
+                                    if (t < t_best && t > kTmin) {
+                                        t_best = t;
+                                        hit = (int)i;
+                                    }
+                                }
+                            }
+                        } else {  // *Rect::Hit
+                            const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
+                            const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
+                            const float t = (p0.x - ok) * (1.0f / dk);
+                            if (!(t < kTmin || t > t_best)) {
+                                const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+                                const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+                                const float xx = oa + t * da;
+                                const float yy = ob + t * db;
+                                if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
+                                    t_best = t;
+                                    hit = (int)i;
+                                }
+                            }
+                        }
+                    }
+                    leaf = 0;
+                    if (node < 0) {  // another leaf was postponed in `node`: process it as well
+                        leaf = node;
+                        node = sp ? (int)stk[(--sp) * BLOCK] : kSentinel;
+                    }
+                }
+                if ((uint32_t)__popcll(__ballot(1)) < threshold) break;  // regenerate finished lanes
+            }
+            if (node == kSentinel && leaf == 0) mode = MODE_SHADE;
+        }
+        if (mode == MODE_SHADE) {
+            f3 contrib;
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            if (shade(&P, prims, hit, t_best, ro, rd, att, rng, rtl, contrib)) {
+                next_sample(contrib);
+            } else if (++depth >= P.max_depth) {
+                next_sample(mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+            } else {
+                start_trace();
+            }
+        }
+        if (__ballot(mode != MODE_DONE) == 0) break;
+    }
+    finish_pixel<COUNT_TESTS>(P, pix, st, rng, col, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v3: v2's resumable traversal with the register footprint cut for occupancy.
+//   * one wave per workgroup (no intra-workgroup coupling of wave lifetimes);
+//   * per-lane path state that only shading needs (cuRAND state, colour sum, attenuation, sample and
+//     depth counters) is parked in LDS while the lane traverses, and the ray's reciprocal direction /
+//     |d|² are recomputed on entry to the traversal phase: only the ray, the traversal cursor and the
+//     closest hit stay in VGPRs across phases;
+//   * 16-bit traversal stack entries in LDS (node and leaf references fit a signed 16 bits when the
+//     scene has < 32767 nodes and < 8192 primitives; rt_render falls back to v2 otherwise);
+//   * the lane's ray count is parked with the path state; primary samples = spp per pixel.
+// LDS per wave: 15 × 256 B of parked state + (depth + 3) × 128 B of stack (2 sentinel pads).
+// ---------------------------------------------------------------------------------------------------
+constexpr int kSentinel16 = 0x7fff;
+constexpr uint32_t kStackBase = 2;  // v3 stack entries start above two sentinel pads
+enum ParkSlot { PK_RNG = 0, PK_COL = 6, PK_ATT = 9, PK_SAMPLE = 12, PK_DEPTH = 13, PK_RAYS = 14, PK_WORDS = 15 };
+
+// Traversal cursor of one lane (v3).
+struct Cursor {
+    int node, leaf, hit;
+    uint32_t sp;
+    float t_best;
+    int mode;
+};
+
+__device__ __forceinline__ void v3_start_trace(uint32_t num_nodes, Cursor& c, uint32_t& rays) {
+    rays++;
+    c.t_best = FLT_MAX;
+    c.hit = -1;
+    c.node = num_nodes ? 0 : kSentinel16;
+    c.leaf = 0;
+    c.sp = kStackBase;
+    c.mode = MODE_TRAV;
+}
+
+// A path ended with `contrib`: accumulate (Kernel.cu:147), then the next sample's camera ray, or finish.
+__device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uint32_t g, f3 contrib, Rng& rng,
+                                               f3& col, f3& att, uint32_t& sample, uint32_t& depth, f3& ro,
+                                               f3& rd, Cursor& c, uint32_t& rays) {
+    col = add(col, contrib);
+    KParamsC* q = kparams_reload();
+    const Camera cam = lane_camera(q, x, g);
+    while (++sample < P.spp) {
+        camera_ray(q, cam, rng, ro, rd);
+        att = mk(1.0f, 1.0f, 1.0f);
+        depth = 0;
+        if (P.max_depth > 0) {
+            v3_start_trace(P.num_nodes, c, rays);
+            return;
+        }
+        col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+    }
+    c.mode = MODE_DONE;
+}
+
+__device__ __forceinline__ void v3_park(uint32_t* park, const Rng& rng, f3 col, f3 att, uint32_t sample,
+                                        uint32_t depth, uint32_t rays) {
+    park[PK_RAYS * 64] = rays;
+    park[(PK_RNG + 0) * 64] = rng.d;
+    park[(PK_RNG + 1) * 64] = rng.v0;
+    park[(PK_RNG + 2) * 64] = rng.v1;
+    park[(PK_RNG + 3) * 64] = rng.v2;
+    park[(PK_RNG + 4) * 64] = rng.v3;
+    park[(PK_RNG + 5) * 64] = rng.v4;
+    park[(PK_COL + 0) * 64] = __float_as_uint(col.x);
+    park[(PK_COL + 1) * 64] = __float_as_uint(col.y);
+    park[(PK_COL + 2) * 64] = __float_as_uint(col.z);
+    park[(PK_ATT + 0) * 64] = __float_as_uint(att.x);
+    park[(PK_ATT + 1) * 64] = __float_as_uint(att.y);
+    park[(PK_ATT + 2) * 64] = __float_as_uint(att.z);
+    park[PK_SAMPLE * 64] = sample;
+    park[PK_DEPTH * 64] = depth;
+}
+
+__device__ __forceinline__ void v3_unpark(const uint32_t* park, Rng& rng, f3& col, f3& att, uint32_t& sample,
+                                          uint32_t& depth, uint32_t& rays) {
+    rays = park[PK_RAYS * 64];
+    rng = Rng{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
+              park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
+    col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
+             __uint_as_float(park[(PK_COL + 2) * 64]));
+    att = mk(__uint_as_float(park[(PK_ATT + 0) * 64]), __uint_as_float(park[(PK_ATT + 1) * 64]),
+             __uint_as_float(park[(PK_ATT + 2) * 64]));
+    sample = park[PK_SAMPLE * 64];
+    depth = park[PK_DEPTH * 64];
+}
+
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
+    extern __shared__ float4 lds[];
+    uint32_t* const park = (uint32_t*)lds + threadIdx.x;                                 // word k: park[k * 64]
+    int16_t* const stk = reinterpret_cast<int16_t*>((uint32_t*)lds + PK_WORDS * 64) + threadIdx.x;  // stk[j * 64]
+    const float4* __restrict__ nodes = P.nodes;
+    const float4* __restrict__ prims = P.prims;
+    uint32_t x, g;
+    size_t pix;
+    if (!lane_pixel<64>(P, x, g, pix)) return;
+    const bool rtl = P.rius_rtl != 0;
+    stk[0] = (int16_t)kSentinel16;  // two sentinel pads below the stack: popping an empty stack yields
+    stk[64] = (int16_t)kSentinel16;  // kSentinel16 without a bounds test
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    Cursor c{kSentinel16, 0, -1, 0u, FLT_MAX, MODE_DONE};
+
+    {  // first camera ray of the pixel
+        uint32_t* st = P.state + pix * 12;
+        Rng rng = load_rng(st);
+        f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
+        uint32_t sample = (uint32_t)-1, depth = 0, rays = 0;
+        if (P.spp > 0) v3_next_sample(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
+        v3_park(park, rng, col, att, sample, depth, rays);  // (col + 0 = +0 above)
+    }
+    const uint32_t threshold = P.regen_threshold;
+
+    while (true) {
+        if (c.mode == MODE_TRAV) {
+            int node = c.node, leaf = c.leaf, hit = c.hit;
+            uint32_t sp = c.sp;
+            float t_best = c.t_best;
+            const float a_dd = dot(rd, rd);
+            const f3 invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
+                               fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
+                               fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
+            const f3 oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
+            while (node != kSentinel16 || leaf < 0) {
+                while ((uint32_t)node < (uint32_t)kSentinel16) {
+                    const int top1 = stk[(sp - 1u) * 64];
+                    const int top2 = stk[(sp - 2u) * 64];
+                    const float4 n0 = nodes[4 * node + 0];
+                    const float4 n1 = nodes[4 * node + 1];
+                    const float4 n2 = nodes[4 * node + 2];
+                    const float4 n3 = nodes[4 * node + 3];
+                    const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
+                    const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
+                    const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
+                    const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
+                    const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
+                    const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
+                    const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+                    const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+                    const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+                    const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+                    if (COUNT_TESTS) {
+                        cnt.boxes += 2;
+                        cnt.wnode += wave_leader();
+                    }
+                    const bool h0 = c0min <= c0max;
+                    const bool h1 = c1min <= c1max;
+                    const bool both = h0 && h1, none = !(h0 || h1);
+                    const bool swap = c1min < c0min;
+                    const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+                    const int nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
+                    const int farc = swap ? ch0 : ch1;
+                    stk[sp * 64] = (int16_t)farc;
+                    int nxt = none ? top1 : nearc;
+                    uint32_t nsp = sp + (both ? 1u : 0u) - ((none && sp > kStackBase) ? 1u : 0u);
+                    // first leaf: postpone it and pop the next entry (the stack top after this visit)
+                    const bool postpone = nxt < 0 && leaf == 0;
+                    const int after_top = both ? farc : (none ? top2 : top1);
+                    leaf = postpone ? nxt : leaf;
+                    nxt = postpone ? after_top : nxt;
+                    nsp = (postpone && nsp > kStackBase) ? nsp - 1u : nsp;
+                    node = nxt;
+                    sp = nsp;
+                    if (__ballot(leaf == 0) == 0) break;
+                }
+                while (leaf < 0) {
+                    const uint32_t l = ~(uint32_t)leaf;
+                    const uint32_t first = l >> 2, count = (l & 3u) + 1u;
+                    for (uint32_t i = first; i < first + count; i++) {
+                        const float4 p0 = prims[2 * i + 0];
+                        const float4 p1 = prims[2 * i + 1];
+                        const uint32_t type = __float_as_uint(p1.w) & 15u;
+                        if (COUNT_TESTS) {
+                            cnt.prims++;
+                            cnt.wleaf += wave_leader();
+                        }
+                        if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                            const f3 oc = sub(ro, xyz(p0));
+                            const float b = dot(oc, rd);
+                            const float c = dot(oc, oc) - p1.x;
+                            const float disc = b * b - a_dd * c;
+                            if (disc > 0) {
+                                const float sq = sqrtf(disc);
+                                float t = (-b - sq) / a_dd;
+                                if (t < t_best && t > kTmin) {
+                                    t_best = t;
+                                    hit = (int)i;
+                                } else {
+                                    t = (-b + sq) / a_dd;
+                                    if (t < t_best && t > kTmin) {
+                                        t_best = t;
+                                        hit = (int)i;
+                                    }
+                                }
+                            }
+                        } else {  // *Rect::Hit
+                            const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
+                            const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
+                            const float t = (p0.x - ok) * (1.0f / dk);
+                            if (!(t < kTmin || t > t_best)) {
+                                const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+                                const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+                                const float xx = oa + t * da;
+                                const float yy = ob + t * db;
+                                if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
+                                    t_best = t;
+                                    hit = (int)i;
+                                }
+                            }
+                        }
+                    }
+                    leaf = 0;
+                    if (node < 0) {
+                        leaf = node;
+                        node = stk[(sp - 1u) * 64];
+                        sp = sp > kStackBase ? sp - 1u : kStackBase;
+                    }
+                }
+                if ((uint32_t)__popcll(__ballot(1)) < threshold) break;
+            }
+            c.node = node;
+            c.leaf = leaf;
+            c.hit = hit;
+            c.sp = sp;
+            c.t_best = t_best;
+            if (c.node == kSentinel16 && c.leaf == 0) c.mode = MODE_SHADE;
+        }
+        if (c.mode == MODE_SHADE) {
+            Rng rng;
+            f3 col, att;
+            uint32_t sample, depth, rays;
+            v3_unpark(park, rng, col, att, sample, depth, rays);
+            f3 contrib;
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.t_best, ro, rd, att, rng, rtl, contrib);
+            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+                ended = true;
+                contrib = mk(0.0f, 0.0f, 0.0f);
+            }
+            if (ended) {
+                v3_next_sample(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
+            } else {
+                v3_start_trace(P.num_nodes, c, rays);
+            }
+            v3_park(park, rng, col, att, sample, depth, rays);
+        }
+        if (__ballot(c.mode != MODE_DONE) == 0) break;
+    }
+    Rng rng;
+    f3 col, att;
+    uint32_t sample, depth, rays;
+    v3_unpark(park, rng, col, att, sample, depth, rays);
+    cnt.rays = rays;
+    cnt.primary = P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
+    finish_pixel<COUNT_TESTS>(P, pix, P.state + pix * 12, rng, col, cnt);
 }
 
 // RenderInit (Kernel.cu:166-176): curand_init(seed_base + global_pixel_index, 0, 0).
@@ -592,13 +1132,20 @@ struct Variant {
     int stack;
     int waves;      // __launch_bounds__ minimum waves per SIMD (1 = compiler's choice)
     int lds_depth;  // LDS stack entries per lane
+    bool resumable; // render_kernel_v2
+    int block;      // threads per workgroup
 };
 
 // rt_set_variant(i) selects kVariants[i]
 constexpr Variant kVariants[] = {
-    {false, dev::STACK_SCRATCH, 1, 0}, {false, dev::STACK_LDS, 1, 24}, {false, dev::STACK_HYBRID, 1, 0},
-    {true, dev::STACK_SCRATCH, 1, 0},  {true, dev::STACK_LDS, 1, 24},  {true, dev::STACK_HYBRID, 1, 0},
-    {false, dev::STACK_LDS, 6, 20},    {false, dev::STACK_LDS, 8, 16},
+    {false, dev::STACK_SCRATCH, 1, 0, false, 256}, {false, dev::STACK_LDS, 1, 24, false, 256},
+    {false, dev::STACK_HYBRID, 1, 0, false, 256},  {true, dev::STACK_SCRATCH, 1, 0, false, 256},
+    {true, dev::STACK_LDS, 1, 24, false, 256},     {true, dev::STACK_HYBRID, 1, 0, false, 256},
+    {false, dev::STACK_LDS, 6, 20, false, 256},    {false, dev::STACK_LDS, 8, 16, false, 256},
+    {false, dev::STACK_LDS, 1, 24, true, 256},     {false, dev::STACK_LDS, 6, 20, true, 256},
+    {false, dev::STACK_LDS, 8, 16, true, 256},     {false, dev::STACK_LDS, 1, 24, true, 64},
+    {false, dev::STACK_LDS, 6, 24, true, 64},     {false, dev::STACK_LDS16, 1, 0, true, 64},
+    {false, dev::STACK_LDS16, 6, 0, true, 64},     {false, dev::STACK_LDS16, 8, 0, true, 64},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -607,7 +1154,13 @@ KernelFn pick_count(bool count) {
     return count ? dev::render_kernel<L, S, true, W> : dev::render_kernel<L, S, false, W>;
 }
 
-KernelFn pick(int variant, bool count) {
+template <int W>
+KernelFn v3_pick(bool count, bool tex) {
+    if (tex) return count ? dev::render_kernel_v3<true, W, true> : dev::render_kernel_v3<false, W, true>;
+    return count ? dev::render_kernel_v3<true, W, false> : dev::render_kernel_v3<false, W, false>;
+}
+
+KernelFn pick(int variant, bool count, bool tex) {
     switch (variant) {
     case 0: return pick_count<false, dev::STACK_SCRATCH, 1>(count);
     case 1: return pick_count<false, dev::STACK_LDS, 1>(count);
@@ -616,9 +1169,19 @@ KernelFn pick(int variant, bool count) {
     case 4: return pick_count<true, dev::STACK_LDS, 1>(count);
     case 5: return pick_count<true, dev::STACK_HYBRID, 1>(count);
     case 6: return pick_count<false, dev::STACK_LDS, 6>(count);
-    default: return pick_count<false, dev::STACK_LDS, 8>(count);
+    case 7: return pick_count<false, dev::STACK_LDS, 8>(count);
+    case 8: return count ? dev::render_kernel_v2<true, 1, 256> : dev::render_kernel_v2<false, 1, 256>;
+    case 9: return count ? dev::render_kernel_v2<true, 6, 256> : dev::render_kernel_v2<false, 6, 256>;
+    case 10: return count ? dev::render_kernel_v2<true, 8, 256> : dev::render_kernel_v2<false, 8, 256>;
+    case 11: return count ? dev::render_kernel_v2<true, 1, 64> : dev::render_kernel_v2<false, 1, 64>;
+    case 12: return count ? dev::render_kernel_v2<true, 6, 64> : dev::render_kernel_v2<false, 6, 64>;
+    case 13: return v3_pick<1>(count, tex);
+    case 14: return v3_pick<6>(count, tex);
+    default: return v3_pick<8>(count, tex);
     }
 }
+
+thread_local int g_regen_threshold = 40;
 
 constexpr size_t kLdsLimit = 160 * 1024;
 
@@ -643,6 +1206,29 @@ int rt_set_variant(int variant) {
     int prev = g_variant;
     g_variant = variant;
     return prev;
+}
+
+int rt_set_tuning(int key, int value) {
+    if (key == RT_TUNE_REGEN_THRESHOLD) {
+        if (value < 1 || value > 64) {
+            set_error("rt_set_tuning: regen threshold must be in [1, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_regen_threshold;
+        g_regen_threshold = value;
+        return prev;
+    }
+    if (key == RT_TUNE_LEAF_MAX) {
+        if (value < 1 || value > kLeafMax) {
+            set_error("rt_set_tuning: leaf max must be in [1, 4]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_leaf_max;
+        g_leaf_max = value;
+        return prev;
+    }
+    set_error("rt_set_tuning: unknown key");
+    return RT_ERR_INVALID_ARGUMENT;
 }
 
 int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) {
@@ -692,11 +1278,12 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.num_ranks = T.num_ranks;
     P.rank = T.rank;
     P.local_rows = T.local_rows;
-    P.tiles_x = (a->width + 15) / 16;
+    P.tiles_x = 0;  // set below for the chosen workgroup shape
     const bool faithful = (a->flags & RT_FLAG_FAITHFUL_GRID) != 0;
     P.grid_w = faithful ? (a->width / 16) * 16 : a->width;
     P.grid_h = faithful ? (a->height / 16) * 16 : a->height;
     P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
+    P.regen_threshold = (uint32_t)g_regen_threshold;
     // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
     const rt_input_struct& in = a->inputs;
     P.width_f = (float)a->width;
@@ -737,6 +1324,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     int variant = g_variant;
     if (variant < 0 || variant >= kNumVariants)  // auto: fastest measured (profiles/r01_*) that fits the BVH
         variant = S.depth <= (uint32_t)kVariants[6].lds_depth + 1 ? 6 : 0;
+    if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
+        variant = 8;  // 16-bit stack references do not fit: resumable kernel with 32-bit stacks
     const Variant& V = kVariants[variant];
     // near-first traversal holds at most one deferred child per level below the root
     if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
@@ -744,13 +1333,16 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         return RT_ERR_UNSUPPORTED;
     }
     size_t lds_bytes = (V.scene_lds ? scene_lds : 0) +
-                       (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * dev::kBlock * 4 : 0);
+                       (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) +
+                       (V.stack == dev::STACK_LDS16 ? (size_t)dev::PK_WORDS * 64 * 4 + (size_t)(S.depth + 3) * 64 * 2 : 0);
     if (lds_bytes > kLdsLimit) {
         set_error("rt_render: scene does not fit in LDS for this variant");
         return RT_ERR_UNSUPPORTED;
     }
-    KernelFn fn = pick(variant, count_tests);
-    const uint32_t tiles = P.tiles_x * ((T.local_rows + 15) / 16);
+    KernelFn fn = pick(variant, count_tests, S.has_textures);
+    const uint32_t tile = V.block == 64 ? 8u : 16u;
+    P.tiles_x = (a->width + tile - 1) / tile;
+    const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing) {
@@ -759,7 +1351,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         (void)hipEventRecord(e0, s);
     }
     (void)hipGetLastError();
-    hipLaunchKernelGGL(fn, dim3(tiles), dim3(dev::kBlock), lds_bytes, s, P);
+    hipLaunchKernelGGL(fn, dim3(tiles), dim3(V.block), lds_bytes, s, P);
     int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
     if (g_timing) {
         (void)hipEventRecord(e1, s);

@@ -7,7 +7,8 @@
 //               n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
 //               n1 = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
 //               n2 = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
-//               n3 = (int c0, int c1, 0, 0)    child >= 0: internal node; child < 0: leaf ~(first<<4 | count)
+//               n3 = (int c0, int c1, 0, 0)    child >= 0: internal node; child < 0: leaf ~(first<<2 | count-1)
+//               (count 1..4; with < 32767 nodes and < 8192 primitives every reference fits a signed 16 bits)
 //   prims   : 2 × float4 = 32 B per primitive, in BVH leaf order:
 //               sphere: p0 = (cx, cy, cz, r),         p1 = (r·r, 0, 0, bits(type | mat << 4))
 //               rect  : p0 = (k, a0, a1, b0),         p1 = (b1, 0, 0, bits(type | mat << 4))
@@ -32,7 +33,8 @@
 
 namespace rt {
 
-constexpr int kLeafMax = 4;         // max primitives per leaf
+constexpr int kLeafMax = 4;         // max primitives per leaf (2-bit count in the leaf reference)
+extern thread_local int g_leaf_max;  // rt_set_tuning(RT_TUNE_LEAF_MAX): 1..kLeafMax, read by the BVH build
 constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) traversal stack
 
 struct HostScene {
@@ -46,6 +48,7 @@ struct HostScene {
     uint32_t num_mats = 0;
     uint32_t depth = 0;          // max root-to-leaf node count
     bool has_image_textures = false;
+    bool has_textures = false;  // any CHECKER or IMAGE albedo
     std::vector<int32_t> prim_source;  // desc index of each primitive (BVH order)
 };
 

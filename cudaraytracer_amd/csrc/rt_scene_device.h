@@ -15,6 +15,7 @@ struct DeviceScene {
     const void* texels = nullptr;  // RGB8
     uint32_t num_nodes = 0, num_prims = 0, num_mats = 0, depth = 0;
     bool has_image_textures = false;
+    bool has_textures = false;  // any CHECKER or IMAGE albedo (selects the texture-capable kernel)
     uint64_t device_bytes = 0;
 };
 

@@ -78,6 +78,7 @@ struct BuildPrim {
 };
 
 struct Builder {
+    int leaf_max = kLeafMax;
     std::vector<BuildPrim> prims;
     std::vector<int> order;  // final primitive order
     struct Node {
@@ -94,7 +95,8 @@ struct Builder {
         return r;
     }
 
-    int make_leaf(int b, int e) const { return ~((b << 4) | (e - b)); }
+    // leaf reference: ~(first << 2 | (count - 1)), count in 1..4 (rt_internal.h)
+    int make_leaf(int b, int e) const { return ~((b << 2) | (e - b - 1)); }
 
     // Returns the child reference for [b, e).
     int build(int b, int e, uint32_t depth) {
@@ -127,7 +129,7 @@ struct Builder {
         Box all = range_box(b, e);
         float leaf_cost = all.area() * (float)n;
         const float kTraversal = 1.2f;  // cost of one node visit relative to one primitive test
-        if (!must_split && n <= kLeafMax && best_cost + kTraversal * all.area() >= leaf_cost) return make_leaf(b, e);
+        if (!must_split && n <= leaf_max && best_cost + kTraversal * all.area() >= leaf_cost) return make_leaf(b, e);
         std::stable_sort(order.begin() + b, order.begin() + e, [&](int x, int y) {
             return prims[x].centroid[best_axis] < prims[y].centroid[best_axis];
         });
@@ -177,6 +179,8 @@ int check_texture(const rt_texture_desc& t, uint32_t num_images, std::string* er
 
 }  // namespace
 
+thread_local int g_leaf_max = kLeafMax;
+
 int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images, std::vector<float>* out,
                    std::string* err) {
     out->assign((size_t)n * 12, 0.0f);
@@ -219,6 +223,9 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
     for (uint32_t i = 0; i < desc->num_materials; i++)
         if (desc->materials[i].type != RT_DIELECTRIC && desc->materials[i].albedo.type == RT_IMAGE)
             out->has_image_textures = true;
+    for (uint32_t i = 0; i < desc->num_materials; i++)
+        if (desc->materials[i].type != RT_DIELECTRIC && desc->materials[i].albedo.type != RT_CONSTANT)
+            out->has_textures = true;
 
     // images
     size_t off = 0;
@@ -241,6 +248,7 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
     }
 
     Builder B;
+    B.leaf_max = g_leaf_max;
     for (uint32_t i = 0; i < desc->num_hittables; i++) {
         const rt_hittable_desc& h = desc->hittables[i];
         if (!h.is_active) continue;  // thrust::remove_if of inactive objects (Hittable.cuh:311-312)

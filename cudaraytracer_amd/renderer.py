@@ -81,7 +81,7 @@ class Renderer:
         # InitCudaBuffers (CudaLayer.cpp:68-74): RGBA8 framebuffer + one 48-byte curandState per pixel
         self.pos = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.state = torch.zeros(n * abi.STATE_WORDS, dtype=torch.int32, device=self.device)
-        self.counters = torch.zeros(4, dtype=torch.int64, device=self.device)
+        self.counters = torch.zeros(8, dtype=torch.int64, device=self.device)
         self.radiance = None
         self.accum = None
 

@@ -226,7 +226,9 @@ typedef struct rt_render_args {
     float* radiance;          /* optional device float[local_rows·width·4]: pre-gamma mean colour (col/spp) */
     float* accum;             /* RT_FLAG_ACCUMULATE: device float4 running sum of samples */
     rt_curand_state* state;   /* device RNG states, local_rows × width */
-    uint64_t* counters;       /* optional device uint64[4]: rays, box tests, primitive tests, primary */
+    uint64_t* counters;       /* optional device uint64[8]: rays, box tests, primitive tests, primary samples;
+                                 with RT_FLAG_COUNT_TESTS also [4..6] = wave-level iterations of node visits,
+                                 primitive tests and shading (SIMD-efficiency diagnostics) */
     uint32_t width;
     uint32_t height;          /* global image height */
     uint32_t samples_per_pixel;
@@ -248,6 +250,13 @@ float rt_last_kernel_ms(void);
 /* Tuning/benchmark knob (per thread): -1 = automatic; 0..5 = (scene tables staged in LDS) * 3 + traversal
  * stack kind (0 = scratch, 1 = LDS, 2 = 4 VGPRs + scratch).  Returns the previous value. */
 int rt_set_variant(int variant);
+
+/* Tuning knob (per thread); returns the previous value or a negative rt_status.
+ *   RT_TUNE_REGEN_THRESHOLD: resumable kernels leave traversal to shade/regenerate finished lanes when
+ *   fewer than this many of a wave's 64 lanes are still tracing (1..64, default 40). */
+/*   RT_TUNE_LEAF_MAX: maximum primitives per BVH leaf used by later rt_scene_create calls (1..4, default 4). */
+enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1 };
+int rt_set_tuning(int key, int value);
 
 /* Host-side helpers (no device needed). */
 

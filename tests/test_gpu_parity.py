@@ -23,7 +23,7 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7]
+VARIANTS = list(range(16))
 
 
 @pytest.fixture(autouse=True)

@@ -98,7 +98,7 @@ def test_bvh_covers_every_active_primitive_once_with_conservative_boxes(which):
         assert depth <= info.depth
         if child < 0:
             leaf = ~child
-            first, count = leaf >> 4, leaf & 15
+            first, count = leaf >> 2, (leaf & 3) + 1
             assert 1 <= count <= 4
             for i in range(first, first + count):
                 seen.append(i)

@@ -11,32 +11,44 @@ ap.add_argument("--config", default="c2")
 ap.add_argument("--variants", default="1,6,7")
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--spp", type=int, default=0)
+ap.add_argument("--thresholds", default="40", help="regen thresholds to try for resumable variants (>= 8)")
+ap.add_argument("--leafmax", default="4", help="BVH leaf sizes to try (RT_TUNE_LEAF_MAX)")
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 if args.spp:
     cfg = cfg.scaled(cfg.width, cfg.height, args.spp)
-variants = [int(v) for v in args.variants.split(",")]
-ds = DeviceScene(scenes.builtin(cfg.scene))
+variants = []
+for lm in (int(x) for x in args.leafmax.split(",")):
+    for v in (int(v) for v in args.variants.split(",")):
+        for th in ([int(t) for t in args.thresholds.split(",")] if v >= 8 else [40]):
+            variants.append((v, th, lm))
+scenes_by_lm = {}
+for lm in sorted({v[2] for v in variants}):
+    lib().rt_set_tuning(1, lm)
+    scenes_by_lm[lm] = DeviceScene(scenes.builtin(cfg.scene))
+lib().rt_set_tuning(1, 4)
 r = Renderer(cfg.width, cfg.height)
 r.render_init()
 inp = cfg.inputs()
 times = {v: [] for v in variants}
 rays = {}
-for v in variants:  # warm-up / JIT of each variant
+for v, th, lm in variants:  # warm-up / JIT of each variant
     lib().rt_set_variant(v)
-    r.render(ds, cfg.spp, cfg.depth, inp)
+    lib().rt_set_tuning(0, th)
+    r.render(scenes_by_lm[lm], cfg.spp, cfg.depth, inp)
 torch.cuda.synchronize()
 for rnd in range(args.rounds):
     for v in variants:
-        lib().rt_set_variant(v)
+        lib().rt_set_variant(v[0])
+        lib().rt_set_tuning(0, v[1])
         r.counters.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        r.render(ds, cfg.spp, cfg.depth, inp)
+        r.render(scenes_by_lm[v[2]], cfg.spp, cfg.depth, inp)
         e1.record()
         torch.cuda.synchronize()
         times[v].append(e0.elapsed_time(e1))
         rays[v] = int(r.counters[0])
 for v in variants:
     med = statistics.median(times[v])
-    print(f"{args.config} variant {v}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)
+    print(f"{args.config} variant {v[0]} thr {v[1]} leafmax {v[2]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)
