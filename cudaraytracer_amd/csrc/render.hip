@@ -1322,10 +1322,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
     const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
     int variant = g_variant;
-    if (variant < 0 || variant >= kNumVariants)  // auto: fastest measured (profiles/r01_*) that fits the BVH
-        variant = S.depth <= (uint32_t)kVariants[6].lds_depth + 1 ? 6 : 0;
+    if (variant < 0 || variant >= kNumVariants)  // auto: fastest measured (profiles/r01_ab_*): v3
+        variant = 13;
     if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
-        variant = 8;  // 16-bit stack references do not fit: resumable kernel with 32-bit stacks
+        variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
     const Variant& V = kVariants[variant];
     // near-first traversal holds at most one deferred child per level below the root
     if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
