@@ -35,6 +35,9 @@ static int upload(const std::vector<T>& host, void** dev, const char* what) {
 
 static void free_device(DeviceScene* s) {
     if (s->nodes) (void)hipFree((void*)s->nodes);
+    if (s->nodes48) (void)hipFree((void*)s->nodes48);
+    if (s->refs16) (void)hipFree((void*)s->refs16);
+    s->nodes48 = s->refs16 = nullptr;
     if (s->prims) (void)hipFree((void*)s->prims);
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);
@@ -52,6 +55,10 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     void* p;
     if ((rc = upload(h.nodes, &p, "hipMalloc/hipMemcpy(nodes)"))) goto fail;
     d.nodes = p;
+    if ((rc = upload(h.nodes48, &p, "hipMalloc/hipMemcpy(nodes48)"))) goto fail;
+    d.nodes48 = p;
+    if ((rc = upload(h.refs16, &p, "hipMalloc/hipMemcpy(refs16)"))) goto fail;
+    d.refs16 = p;
     if ((rc = upload(h.prims, &p, "hipMalloc/hipMemcpy(prims)"))) goto fail;
     d.prims = p;
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;

@@ -95,6 +95,8 @@ __device__ __forceinline__ f3 random_in_unit_sphere(Rng& s, bool rtl) {
 // ---------------------------------------------------------------------------------------------------
 struct KParams {
     const float4* nodes;
+    const float4* nodes48;   // v3: three box float4 per node
+    const uint32_t* refs16;  // v3: packed 16-bit child references
     const float4* prims;
     const float4* mats;
     const int4* imgs;
@@ -905,7 +907,12 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     extern __shared__ float4 lds[];
     uint32_t* const park = (uint32_t*)lds + threadIdx.x;                                 // word k: park[k * 64]
     int16_t* const stk = reinterpret_cast<int16_t*>((uint32_t*)lds + PK_WORDS * 64) + threadIdx.x;  // stk[j * 64]
-    const float4* __restrict__ nodes = P.nodes;
+    // node boxes and packed child references through buffer descriptors: 32-bit offsets, no 64-bit
+    // address arithmetic per visit; 48 B of boxes + 4 B of references per node
+    const __amdgpu_buffer_rsrc_t nrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
     const float4* __restrict__ prims = P.prims;
     uint32_t x, g;
     size_t pix;
@@ -942,10 +949,11 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
                 while ((uint32_t)node < (uint32_t)kSentinel16) {
                     const int top1 = stk[(sp - 1u) * 64];
                     const int top2 = stk[(sp - 2u) * 64];
-                    const float4 n0 = nodes[4 * node + 0];
-                    const float4 n1 = nodes[4 * node + 1];
-                    const float4 n2 = nodes[4 * node + 2];
-                    const float4 n3 = nodes[4 * node + 3];
+                    const uint32_t noff = (uint32_t)node * 48u;
+                    const float4 n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
+                    const float4 n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
+                    const float4 n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
+                    const uint32_t refs = __builtin_amdgcn_raw_buffer_load_b32(rrsrc, (uint32_t)node * 4u, 0, 0);
                     const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
                     const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
                     const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
@@ -964,7 +972,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
                     const bool h1 = c1min <= c1max;
                     const bool both = h0 && h1, none = !(h0 || h1);
                     const bool swap = c1min < c0min;
-                    const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+                    const int ch0 = (int)(int16_t)(refs & 0xffffu), ch1 = (int)refs >> 16;
                     const int nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
                     const int farc = swap ? ch0 : ch1;
                     stk[sp * 64] = (int16_t)farc;
@@ -1258,6 +1266,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     dev::KParams P;
     std::memset(&P, 0, sizeof(P));
     P.nodes = (const float4*)S.nodes;
+    P.nodes48 = (const float4*)S.nodes48;
+    P.refs16 = (const uint32_t*)S.refs16;
     P.prims = (const float4*)S.prims;
     P.mats = (const float4*)S.mats;
     P.imgs = (const int4*)S.imgs;

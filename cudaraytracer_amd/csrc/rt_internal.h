@@ -39,6 +39,8 @@ constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) trave
 
 struct HostScene {
     std::vector<float> nodes;   // 16 floats per node
+    std::vector<float> nodes48; // 12 floats per node: the three box float4 of `nodes` (v3 kernels)
+    std::vector<uint32_t> refs16;  // per node: child 0 | child 1 << 16 as signed 16-bit references
     std::vector<float> prims;   // 8 floats per primitive
     std::vector<float> mats;    // 12 floats per material
     std::vector<int32_t> imgs;  // 4 ints per image

@@ -284,6 +284,13 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         o[14] = 0.0f;
         o[15] = 0.0f;
     }
+    out->nodes48.resize((size_t)out->num_nodes * 12);
+    out->refs16.resize(out->num_nodes);
+    for (uint32_t i = 0; i < out->num_nodes; i++) {
+        for (int k = 0; k < 12; k++) out->nodes48[(size_t)i * 12 + k] = out->nodes[(size_t)i * 16 + k];
+        const Builder::Node& n = B.nodes[i];
+        out->refs16[i] = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);  // valid when refs fit int16
+    }
     out->prims.resize((size_t)out->num_prims * 8);
     out->prim_source.resize(out->num_prims);
     for (uint32_t i = 0; i < out->num_prims; i++) {
