@@ -37,7 +37,8 @@ static void free_device(DeviceScene* s) {
     if (s->nodes) (void)hipFree((void*)s->nodes);
     if (s->nodes48) (void)hipFree((void*)s->nodes48);
     if (s->refs16) (void)hipFree((void*)s->refs16);
-    s->nodes48 = s->refs16 = nullptr;
+    if (s->nodes32) (void)hipFree((void*)s->nodes32);
+    s->nodes48 = s->refs16 = s->nodes32 = nullptr;
     if (s->prims) (void)hipFree((void*)s->prims);
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);
@@ -59,6 +60,8 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     d.nodes48 = p;
     if ((rc = upload(h.refs16, &p, "hipMalloc/hipMemcpy(refs16)"))) goto fail;
     d.refs16 = p;
+    if ((rc = upload(h.nodes32, &p, "hipMalloc/hipMemcpy(nodes32)"))) goto fail;
+    d.nodes32 = p;
     if ((rc = upload(h.prims, &p, "hipMalloc/hipMemcpy(prims)"))) goto fail;
     d.prims = p;
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
@@ -73,6 +76,7 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;
+    d.has_half_nodes = h.has_half_nodes;
     d.device_bytes = (h.nodes.size() + h.prims.size() + h.mats.size()) * 4 + h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;
@@ -302,6 +306,21 @@ int rt_build_host_tables(const rt_scene_desc* desc, float* nodes, float* prims, 
     if (prims) std::copy(h.prims.begin(), h.prims.end(), prims);
     if (materials) std::copy(h.mats.begin(), h.mats.end(), materials);
     if (prim_source) std::copy(h.prim_source.begin(), h.prim_source.end(), prim_source);
+    return RT_OK;
+}
+
+int rt_build_host_half_nodes(const rt_scene_desc* desc, uint32_t* nodes32, uint32_t* num_nodes) {
+    if (!num_nodes) { set_error("rt_build_host_half_nodes: num_nodes is NULL"); return RT_ERR_INVALID_ARGUMENT; }
+    HostScene h;
+    std::string err;
+    int rc = build_host_scene(desc, &h, &err);
+    if (rc) { set_error("rt_build_host_half_nodes: " + err); return rc; }
+    *num_nodes = h.num_nodes;
+    if (!h.has_half_nodes) {
+        set_error("rt_build_host_half_nodes: a box plane lies beyond the binary16 range");
+        return RT_ERR_UNSUPPORTED;
+    }
+    if (nodes32) std::copy(h.nodes32.begin(), h.nodes32.end(), nodes32);
     return RT_OK;
 }
 

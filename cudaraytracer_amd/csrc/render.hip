@@ -25,6 +25,7 @@
 #include <cfloat>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 
 #include "rt_internal.h"
@@ -39,6 +40,10 @@ namespace dev {
 struct f3 {
     float x, y, z;
 };
+typedef __fp16 half2v __attribute__((ext_vector_type(2)));
+
+// BVH node layouts read by the v3/v4 traversal (template argument NODES)
+enum NodeLayout { NODES_48 = 0, NODES_HALF = 1, NODES_64 = 2 };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -97,6 +102,7 @@ struct KParams {
     const float4* nodes;
     const float4* nodes48;   // v3: three box float4 per node
     const uint32_t* refs16;  // v3: packed 16-bit child references
+    const uint32_t* nodes32; // v3/v4 HALF: 32-B nodes with binary16 child boxes
     const float4* prims;
     const float4* mats;
     const int4* imgs;
@@ -119,6 +125,8 @@ struct KParams {
     float k10_fwd[3];  // (1.0f / inputs.fov * 10.0f) * forwardV (Kernel.cu:143)
     float bg0[3], bg1[3];
     uint32_t regen_threshold;  // v2: lanes still tracing below which finished lanes are regenerated
+    uint32_t* work_counter;    // v4: the frame's work queue head (zeroed before the launch)
+    uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
 };
 
 constexpr int kStackMax = 64;
@@ -354,9 +362,22 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, Rng& rng, f3
 template <bool TEX = true, class PP>
 __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, int hit, float t, f3& ro,
                                       f3& rd, f3& att, Rng& rng, bool rtl, f3& contrib) {
+    // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
+    // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
+    uint32_t mtype = 0xffu;  // 0xff: miss
+    if (hit >= 0) {
+        const uint32_t tag = __float_as_uint(prims[2 * hit + 1].w);
+        mtype = __float_as_uint(P->mats[3 * (tag >> 4)].x) & 15u;
+    }
+    const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
+    float len = 1.0f;
+    f3 ud = mk(0.0f, 0.0f, 0.0f);
+    if (hit < 0 || specular) {
+        len = length(rd);
+        ud.y = rd.y / len;
+    }
     if (hit < 0) {  // sky (Kernel.cu:41-44)
-        const f3 unit_direction = unit_vector(rd);
-        const float tt = 0.5f * (unit_direction.y + 1.0f);
+        const float tt = 0.5f * (ud.y + 1.0f);
         const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
         contrib = mulv(att, c);
         return true;
@@ -366,8 +387,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
     const uint32_t tag = __float_as_uint(p1.w);
     const uint32_t type = tag & 15u, mat = tag >> 4;
     const float4 m0 = P->mats[3 * mat + 0];
-    const uint32_t mbits = __float_as_uint(m0.x);
-    const uint32_t mtype = mbits & 15u, ttype = (mbits >> 4) & 15u;
+    const uint32_t ttype = (__float_as_uint(m0.x) >> 4) & 15u;
     f3 p, normal;
     float hu = 0.0f, hv = 0.0f;
     if (type == RT_SPHERE) {  // hit record of Sphere::Hit (Hittable.cuh:91-95)
@@ -404,25 +424,28 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         contrib = mulv(e, att);
         return true;
     }
+    if (specular) {
+        ud.x = rd.x / len;
+        ud.z = rd.z / len;
+    }
     if (mtype == RT_DIELECTRIC) {  // Dielectric::Scatter (Material.cuh:106-136); attenuation (1,1,1)
         // Evaluated in an order that keeps few values live: every quantity is the same binary32 value the
         // reference computes (pure functions of rd, normal, ir), and only the chosen direction is formed.
+        // m1 = (1.0f / ir, r0²) precomputed on the host with the same operations (rt_internal.h).
         const float ir = m0.y;
+        const float4 m1 = P->mats[3 * mat + 1];
         const float dn = dot(rd, normal);
-        const float len = length(rd);
         const bool exiting = dn > 0.0f;
         float cosine = (exiting ? dn : -dn) / len;
         if (exiting) cosine = sqrtf(1.0f - ir * ir * (1 - cosine * cosine));
-        const float ni_over_nt = exiting ? ir : 1.0f / ir;
+        const float ni_over_nt = exiting ? ir : m1.x;
         const f3 outward_normal = exiting ? neg(normal) : normal;
-        // Refract (Math.cuh:292-304): uv = UnitVector(v) = v / v.Length()
-        const f3 uv = divs(rd, len);
-        const float dt = dot(uv, outward_normal);
+        // Refract (Math.cuh:292-304): uv = UnitVector(v)
+        const float dt = dot(ud, outward_normal);
         const float discriminant = 1.0f - ni_over_nt * ni_over_nt * (1 - dt * dt);
         float reflect_prob = 1.0f;
-        if (discriminant > 0) {
-            float r0 = (1.0f - ir) / (1.0f + ir);  // Reflectance (Material.cuh:139-145)
-            r0 = r0 * r0;
+        if (discriminant > 0) {  // Reflectance (Material.cuh:139-145)
+            const float r0 = m1.y;
             const float xs = 1.0f - cosine;
             const float x2 = xs * xs;
             reflect_prob = r0 + (1.0f - r0) * ((x2 * x2) * xs);
@@ -431,7 +454,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         if (refl) {
             rd = reflect(rd, normal);
         } else if (discriminant > 0) {
-            rd = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))), scale(sqrtf(discriminant), outward_normal));
+            rd = sub(scale(ni_over_nt, sub(ud, scale(dt, outward_normal))), scale(sqrtf(discriminant), outward_normal));
         } else {
             rd = mk(0.0f, 0.0f, 0.0f);  // uninitialised `refracted` in the reference (ξ = 1.0, TIR)
         }
@@ -446,7 +469,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         const f3 target = add(add(p, normal), q);
         rd = sub(target, p);
     } else {  // Metal::Scatter (Material.cuh:75-94)
-        const f3 reflected = reflect(unit_vector(rd), normal);
+        const f3 reflected = reflect(ud, normal);
         rd = add(reflected, scale(m0.y, q));
         ok = dot(rd, normal) > 0;
     }
@@ -466,9 +489,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
 }
 
 // Pixel epilogue (Kernel.cu:149-157): RNG state store, average, gamma 2, RGBA8 pack; optional outputs.
-template <bool COUNT_TESTS>
-__device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint32_t* st, const Rng& rng, f3 col,
-                                             const Counts& cnt) {
+__device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32_t* st, const Rng& rng, f3 col) {
     if (!(P.flags & RT_FLAG_NO_STATE_WRITEBACK)) {
         *reinterpret_cast<uint4*>(st) = make_uint4(rng.d, rng.v0, rng.v1, rng.v2);
         *reinterpret_cast<uint2*>(st + 4) = make_uint2(rng.v3, rng.v4);
@@ -487,6 +508,10 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint3
     }
     if (P.radiance) P.radiance[pix] = make_float4(c.x, c.y, c.z, 1.0f);
     if (P.pos) P.pos[pix] = rgb_to_int(255.0f * sqrtf(c.x), 255.0f * sqrtf(c.y), 255.0f * sqrtf(c.z));
+}
+
+template <bool COUNT_TESTS>
+__device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt) {
     if (P.counters) {
         atomicAdd(&P.counters[0], (unsigned long long)cnt.rays);
         if (COUNT_TESTS) {
@@ -498,6 +523,13 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint3
         }
         atomicAdd(&P.counters[3], (unsigned long long)cnt.primary);
     }
+}
+
+template <bool COUNT_TESTS>
+__device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint32_t* st, const Rng& rng, f3 col,
+                                             const Counts& cnt) {
+    write_pixel(P, pix, st, rng, col);
+    flush_counts<COUNT_TESTS>(P, cnt);
 }
 
 // Lane → pixel.  BLOCK = 256: a workgroup covers a 16×16 tile, each wave an 8×8 sub-tile (P.tiles_x =
@@ -902,7 +934,154 @@ __device__ __forceinline__ void v3_unpark(const uint32_t* park, Rng& rng, f3& co
     depth = park[PK_DEPTH * 64];
 }
 
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX>
+// Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
+// until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
+// still tracing (the wave then shades the finished lanes and regenerates them).
+template <bool COUNT_TESTS, int NODES>
+__device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, const __amdgpu_buffer_rsrc_t rrsrc,
+                                            const float4* __restrict__ prims, int16_t* const stk,
+                                            const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
+                                            Counts& cnt) {
+    int node = c.node, leaf = c.leaf, hit = c.hit;
+    uint32_t sp = c.sp;
+    float t_best = c.t_best;
+    const float a_dd = dot(rd, rd);
+    const f3 invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
+                       fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
+                       fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
+    const f3 oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
+    while (node != kSentinel16 || leaf < 0) {
+        while ((uint32_t)node < (uint32_t)kSentinel16) {
+            const int top1 = stk[(sp - 1u) * 64];
+            const int top2 = stk[(sp - 2u) * 64];
+            float4 n0, n1, n2;
+            int ch0, ch1;
+            if constexpr (NODES == NODES_HALF) {  // 32-B node: binary16 planes (exact in f32: v_fma_mix_f32) + refs
+                const uint32_t noff = (uint32_t)node << 5;
+                const uint4 q0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
+                const uint4 q1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
+                const half2v h0 = __builtin_bit_cast(half2v, q0.x), h1 = __builtin_bit_cast(half2v, q0.y);
+                const half2v h2 = __builtin_bit_cast(half2v, q0.z), h3 = __builtin_bit_cast(half2v, q0.w);
+                const half2v h4 = __builtin_bit_cast(half2v, q1.x), h5 = __builtin_bit_cast(half2v, q1.y);
+                n0 = make_float4((float)h0.x, (float)h0.y, (float)h1.x, (float)h1.y);
+                n1 = make_float4((float)h2.x, (float)h2.y, (float)h3.x, (float)h3.y);
+                n2 = make_float4((float)h4.x, (float)h4.y, (float)h5.x, (float)h5.y);
+                ch0 = (int)(int16_t)(q1.z & 0xffffu);
+                ch1 = (int)q1.z >> 16;
+            } else if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
+                const uint32_t noff = (uint32_t)node << 6;
+                n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
+                n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
+                n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
+                const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
+                ch0 = (int)r2.x;
+                ch1 = (int)r2.y;
+            } else {  // 48 B of f32 boxes + 4 B of references
+                const uint32_t noff = (uint32_t)node * 48u;
+                n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
+                n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
+                n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
+                const uint32_t refs = __builtin_amdgcn_raw_buffer_load_b32(rrsrc, (uint32_t)node * 4u, 0, 0);
+                ch0 = (int)(int16_t)(refs & 0xffffu);
+                ch1 = (int)refs >> 16;
+            }
+            const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
+            const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
+            const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
+            const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
+            const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
+            const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
+            const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+            const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+            const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+            const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+            if (COUNT_TESTS) {
+                cnt.boxes += 2;
+                cnt.wnode += wave_leader();
+            }
+            const bool h0 = c0min <= c0max;
+            const bool h1 = c1min <= c1max;
+            const bool both = h0 && h1, none = !(h0 || h1);
+            const bool swap = c1min < c0min;
+            const int nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
+            const int farc = swap ? ch0 : ch1;
+            stk[sp * 64] = (int16_t)farc;
+            int nxt = none ? top1 : nearc;
+            uint32_t nsp = sp + (both ? 1u : 0u) - ((none && sp > kStackBase) ? 1u : 0u);
+            // first leaf: postpone it and pop the next entry (the stack top after this visit)
+            const bool postpone = nxt < 0 && leaf == 0;
+            const int after_top = both ? farc : (none ? top2 : top1);
+            leaf = postpone ? nxt : leaf;
+            nxt = postpone ? after_top : nxt;
+            nsp = (postpone && nsp > kStackBase) ? nsp - 1u : nsp;
+            node = nxt;
+            sp = nsp;
+            if (__ballot(leaf == 0) == 0) break;
+        }
+        while (leaf < 0) {
+            const uint32_t l = ~(uint32_t)leaf;
+            const uint32_t first = l >> 2, count = (l & 3u) + 1u;
+            for (uint32_t i = first; i < first + count; i++) {
+                const float4 p0 = prims[2 * i + 0];
+                const float4 p1 = prims[2 * i + 1];
+                const uint32_t type = __float_as_uint(p1.w) & 15u;
+                if (COUNT_TESTS) {
+                    cnt.prims++;
+                    cnt.wleaf += wave_leader();
+                }
+                if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                    const f3 oc = sub(ro, xyz(p0));
+                    const float b = dot(oc, rd);
+                    const float c = dot(oc, oc) - p1.x;
+                    const float disc = b * b - a_dd * c;
+                    if (disc > 0) {
+                        const float sq = sqrtf(disc);
+                        float t = (-b - sq) / a_dd;
+                        if (t < t_best && t > kTmin) {
+                            t_best = t;
+                            hit = (int)i;
+                        } else {
+                            t = (-b + sq) / a_dd;
+                            if (t < t_best && t > kTmin) {
+                                t_best = t;
+                                hit = (int)i;
+                            }
+                        }
+                    }
+                } else {  // *Rect::Hit
+                    const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
+                    const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
+                    const float t = (p0.x - ok) * (1.0f / dk);
+                    if (!(t < kTmin || t > t_best)) {
+                        const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+                        const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+                        const float xx = oa + t * da;
+                        const float yy = ob + t * db;
+                        if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
+                            t_best = t;
+                            hit = (int)i;
+                        }
+                    }
+                }
+            }
+            leaf = 0;
+            if (node < 0) {
+                leaf = node;
+                node = stk[(sp - 1u) * 64];
+                sp = sp > kStackBase ? sp - 1u : kStackBase;
+            }
+        }
+        if ((uint32_t)__popcll(__ballot(1)) < threshold) break;
+    }
+    c.node = node;
+    c.leaf = leaf;
+    c.hit = hit;
+    c.sp = sp;
+    c.t_best = t_best;
+    if (c.node == kSentinel16 && c.leaf == 0) c.mode = MODE_SHADE;
+}
+
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
     extern __shared__ float4 lds[];
     uint32_t* const park = (uint32_t*)lds + threadIdx.x;                                 // word k: park[k * 64]
@@ -910,7 +1089,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     // node boxes and packed child references through buffer descriptors: 32-bit offsets, no 64-bit
     // address arithmetic per visit; 48 B of boxes + 4 B of references per node
     const __amdgpu_buffer_rsrc_t nrsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+        NODES == NODES_HALF ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes32, (short)0, (int)(P.num_nodes * 32u), 0x00020000)
+        : NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+                            : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rrsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
     const float4* __restrict__ prims = P.prims;
@@ -937,118 +1118,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
 
     while (true) {
         if (c.mode == MODE_TRAV) {
-            int node = c.node, leaf = c.leaf, hit = c.hit;
-            uint32_t sp = c.sp;
-            float t_best = c.t_best;
-            const float a_dd = dot(rd, rd);
-            const f3 invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
-                               fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
-                               fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
-            const f3 oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
-            while (node != kSentinel16 || leaf < 0) {
-                while ((uint32_t)node < (uint32_t)kSentinel16) {
-                    const int top1 = stk[(sp - 1u) * 64];
-                    const int top2 = stk[(sp - 2u) * 64];
-                    const uint32_t noff = (uint32_t)node * 48u;
-                    const float4 n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
-                    const float4 n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
-                    const float4 n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
-                    const uint32_t refs = __builtin_amdgcn_raw_buffer_load_b32(rrsrc, (uint32_t)node * 4u, 0, 0);
-                    const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
-                    const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
-                    const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
-                    const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
-                    const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
-                    const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
-                    const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
-                    const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
-                    const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
-                    const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
-                    if (COUNT_TESTS) {
-                        cnt.boxes += 2;
-                        cnt.wnode += wave_leader();
-                    }
-                    const bool h0 = c0min <= c0max;
-                    const bool h1 = c1min <= c1max;
-                    const bool both = h0 && h1, none = !(h0 || h1);
-                    const bool swap = c1min < c0min;
-                    const int ch0 = (int)(int16_t)(refs & 0xffffu), ch1 = (int)refs >> 16;
-                    const int nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
-                    const int farc = swap ? ch0 : ch1;
-                    stk[sp * 64] = (int16_t)farc;
-                    int nxt = none ? top1 : nearc;
-                    uint32_t nsp = sp + (both ? 1u : 0u) - ((none && sp > kStackBase) ? 1u : 0u);
-                    // first leaf: postpone it and pop the next entry (the stack top after this visit)
-                    const bool postpone = nxt < 0 && leaf == 0;
-                    const int after_top = both ? farc : (none ? top2 : top1);
-                    leaf = postpone ? nxt : leaf;
-                    nxt = postpone ? after_top : nxt;
-                    nsp = (postpone && nsp > kStackBase) ? nsp - 1u : nsp;
-                    node = nxt;
-                    sp = nsp;
-                    if (__ballot(leaf == 0) == 0) break;
-                }
-                while (leaf < 0) {
-                    const uint32_t l = ~(uint32_t)leaf;
-                    const uint32_t first = l >> 2, count = (l & 3u) + 1u;
-                    for (uint32_t i = first; i < first + count; i++) {
-                        const float4 p0 = prims[2 * i + 0];
-                        const float4 p1 = prims[2 * i + 1];
-                        const uint32_t type = __float_as_uint(p1.w) & 15u;
-                        if (COUNT_TESTS) {
-                            cnt.prims++;
-                            cnt.wleaf += wave_leader();
-                        }
-                        if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
-                            const f3 oc = sub(ro, xyz(p0));
-                            const float b = dot(oc, rd);
-                            const float c = dot(oc, oc) - p1.x;
-                            const float disc = b * b - a_dd * c;
-                            if (disc > 0) {
-                                const float sq = sqrtf(disc);
-                                float t = (-b - sq) / a_dd;
-                                if (t < t_best && t > kTmin) {
-                                    t_best = t;
-                                    hit = (int)i;
-                                } else {
-                                    t = (-b + sq) / a_dd;
-                                    if (t < t_best && t > kTmin) {
-                                        t_best = t;
-                                        hit = (int)i;
-                                    }
-                                }
-                            }
-                        } else {  // *Rect::Hit
-                            const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
-                            const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
-                            const float t = (p0.x - ok) * (1.0f / dk);
-                            if (!(t < kTmin || t > t_best)) {
-                                const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
-                                const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
-                                const float xx = oa + t * da;
-                                const float yy = ob + t * db;
-                                if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
-                                    t_best = t;
-                                    hit = (int)i;
-                                }
-                            }
-                        }
-                    }
-                    leaf = 0;
-                    if (node < 0) {
-                        leaf = node;
-                        node = stk[(sp - 1u) * 64];
-                        sp = sp > kStackBase ? sp - 1u : kStackBase;
-                    }
-                }
-                if ((uint32_t)__popcll(__ballot(1)) < threshold) break;
-            }
-            c.node = node;
-            c.leaf = leaf;
-            c.hit = hit;
-            c.sp = sp;
-            c.t_best = t_best;
-            if (c.node == kSentinel16 && c.leaf == 0) c.mode = MODE_SHADE;
+            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, prims, stk, threshold, ro, rd, c, cnt);
         }
         if (c.mode == MODE_SHADE) {
             Rng rng;
@@ -1078,6 +1148,146 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     cnt.rays = rays;
     cnt.primary = P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
     finish_pixel<COUNT_TESTS>(P, pix, P.state + pix * 12, rng, col, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v4: v3 made persistent, with per-lane pixel regeneration.
+//   v3 gives each lane one pixel for the wave's lifetime, so a lane whose 64 samples are done idles
+//   until the wave's slowest pixel finishes, and every wave pays a workgroup dispatch.  v4 launches
+//   only as many single-wave workgroups as fit on the device at once; the frame is a queue of work
+//   indices (8×8 tiles in row-major tile order, 64 indices per tile), and a lane that finishes its pixel
+//   takes the next index at once.  The wave pulls 64-index chunks from the frame's counter with one
+//   atomic per chunk; needy lanes take consecutive indices of the wave's chunk (ballot + mbcnt rank).
+//   Every pixel still runs the reference's per-pixel sample loop on its own cuRAND stream, so the
+//   result does not depend on which lane or wave renders it.  Every wave exits once the queue is empty
+//   and its lanes are done (no wave waits on another).
+// Requires spp ≥ 1 and max_depth ≥ 1 (rt_render uses v3 otherwise).
+// LDS per wave: 18 × 256 B of parked state + (depth + 3) × 128 B of stack.
+// ---------------------------------------------------------------------------------------------------
+enum ParkSlotV4 { PK_X = PK_WORDS, PK_G = PK_WORDS + 1, PK_PIX = PK_WORDS + 2, PK_WORDS4 = PK_WORDS + 3 };
+constexpr int MODE_NEED = 3;  // v4: lane waits for a pixel
+
+// Work index → pixel of the local image (8×8 tiles, row-major tile order); false when the index lies
+// outside the image or outside the rendered grid.
+__device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint32_t& x, uint32_t& g, uint32_t& pix) {
+    const uint32_t tile = idx >> 6, l = idx & 63u;
+    const uint32_t by = tile / P.tiles_x, bx = tile - by * P.tiles_x;
+    x = bx * 8u + (l & 7u);
+    const uint32_t ly = by * 8u + (l >> 3);
+    if (x >= P.width || ly >= P.local_rows) return false;
+    g = global_row(P, ly);
+    if (x >= P.grid_w || g >= P.grid_h) return false;
+    pix = ly * P.width + x;
+    return true;
+}
+
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
+    extern __shared__ float4 lds[];
+    uint32_t* const park = (uint32_t*)lds + threadIdx.x;
+    int16_t* const stk = reinterpret_cast<int16_t*>((uint32_t*)lds + PK_WORDS4 * 64) + threadIdx.x;
+    const __amdgpu_buffer_rsrc_t nrsrc =
+        NODES == NODES_HALF ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes32, (short)0, (int)(P.num_nodes * 32u), 0x00020000)
+        : NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+                            : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
+    const float4* __restrict__ prims = P.prims;
+    const bool rtl = P.rius_rtl != 0;
+    stk[0] = (int16_t)kSentinel16;
+    stk[64] = (int16_t)kSentinel16;
+    park[PK_RAYS * 64] = 0u;
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    Cursor c{kSentinel16, 0, -1, 0u, FLT_MAX, MODE_NEED};
+    uint32_t wq_next = 0u, wq_end = 0u;  // wave-uniform: the wave's current chunk of work indices
+    bool drained = false;                // wave-uniform: the frame's queue is empty
+    const uint32_t threshold = P.regen_threshold;
+
+    while (true) {
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, prims, stk, threshold, ro, rd, c, cnt);
+        Rng rng;
+        f3 col, att;
+        uint32_t sample, depth, rays;
+        bool cam = false, fin = false;
+        const bool shading = c.mode == MODE_SHADE;
+        if (shading) {
+            v3_unpark(park, rng, col, att, sample, depth, rays);
+            f3 contrib;
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.t_best, ro, rd, att, rng, rtl, contrib);
+            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+                ended = true;
+                contrib = mk(0.0f, 0.0f, 0.0f);
+            }
+            if (ended) {
+                col = add(col, contrib);  // Kernel.cu:147
+                if (++sample < P.spp) {
+                    cam = true;
+                } else {  // the pixel is done (Kernel.cu:149-157)
+                    const uint32_t pix = park[PK_PIX * 64];
+                    write_pixel(P, pix, P.state + (size_t)pix * 12, rng, col);
+                    fin = true;
+                }
+            } else {
+                v3_start_trace(P.num_nodes, c, rays);
+            }
+        }
+        // pixel regeneration: lanes without a pixel take the next work indices
+        bool need = fin || c.mode == MODE_NEED;
+        uint64_t needm = __ballot(need);
+        if (needm != 0) {
+            if (!shading && need) rays = park[PK_RAYS * 64];
+            while (needm != 0 && !drained) {
+                if (wq_next >= wq_end) {
+                    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+                    uint32_t base = 0u;
+                    if (__lane_id() == leader) base = atomicAdd(P.work_counter, 64u);
+                    base = __builtin_amdgcn_readlane(base, leader);
+                    if (base >= P.work_total) {
+                        drained = true;
+                        break;
+                    }
+                    wq_next = base;
+                    wq_end = base + 64u;
+                }
+                const uint32_t avail = wq_end - wq_next;
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+                if (need && rank < avail) {
+                    uint32_t x, g, pix;
+                    if (work_pixel(P, wq_next + rank, x, g, pix)) {
+                        need = false;
+                        park[PK_X * 64] = x;
+                        park[PK_G * 64] = g;
+                        park[PK_PIX * 64] = pix;
+                        rng = load_rng(P.state + (size_t)pix * 12);
+                        col = mk(0.0f, 0.0f, 0.0f);
+                        sample = 0u;
+                        cnt.primary += P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
+                        cam = true;
+                    }
+                }
+                const uint32_t taken = min((uint32_t)__popcll(needm), avail);
+                wq_next += taken;
+                needm = __ballot(need);
+            }
+            if (need) c.mode = MODE_DONE;
+        }
+        if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
+            KParamsC* q = kparams_reload();
+            const Camera cam_l = lane_camera(q, park[PK_X * 64], park[PK_G * 64]);
+            camera_ray(q, cam_l, rng, ro, rd);
+            att = mk(1.0f, 1.0f, 1.0f);
+            depth = 0u;
+            v3_start_trace(P.num_nodes, c, rays);
+        }
+        if (shading || cam) v3_park(park, rng, col, att, sample, depth, rays);
+        if (__ballot(c.mode != MODE_DONE) == 0) break;
+    }
+    cnt.rays = park[PK_RAYS * 64];
+    flush_counts<COUNT_TESTS>(P, cnt);
 }
 
 // RenderInit (Kernel.cu:166-176): curand_init(seed_base + global_pixel_index, 0, 0).
@@ -1142,6 +1352,8 @@ struct Variant {
     int lds_depth;  // LDS stack entries per lane
     bool resumable; // render_kernel_v2
     int block;      // threads per workgroup
+    bool persistent = false;  // render_kernel_v4: device-filling grid + work queue
+    bool half = false;        // binary16 child boxes (32-B nodes)
 };
 
 // rt_set_variant(i) selects kVariants[i]
@@ -1154,6 +1366,10 @@ constexpr Variant kVariants[] = {
     {false, dev::STACK_LDS, 8, 16, true, 256},     {false, dev::STACK_LDS, 1, 24, true, 64},
     {false, dev::STACK_LDS, 6, 24, true, 64},     {false, dev::STACK_LDS16, 1, 0, true, 64},
     {false, dev::STACK_LDS16, 6, 0, true, 64},     {false, dev::STACK_LDS16, 8, 0, true, 64},
+    {false, dev::STACK_LDS16, 1, 0, true, 64, true}, {false, dev::STACK_LDS16, 6, 0, true, 64, true},
+    {false, dev::STACK_LDS16, 1, 0, true, 64, false, true}, {false, dev::STACK_LDS16, 1, 0, true, 64, true, true},
+    {false, dev::STACK_LDS16, 6, 0, true, 64, true, true},
+    {false, dev::STACK_LDS16, 1, 0, true, 64}, {false, dev::STACK_LDS16, 1, 0, true, 64, true},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -1162,10 +1378,16 @@ KernelFn pick_count(bool count) {
     return count ? dev::render_kernel<L, S, true, W> : dev::render_kernel<L, S, false, W>;
 }
 
-template <int W>
+template <int W, int H = dev::NODES_48>
 KernelFn v3_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v3<true, W, true> : dev::render_kernel_v3<false, W, true>;
-    return count ? dev::render_kernel_v3<true, W, false> : dev::render_kernel_v3<false, W, false>;
+    if (tex) return count ? dev::render_kernel_v3<true, W, true, H> : dev::render_kernel_v3<false, W, true, H>;
+    return count ? dev::render_kernel_v3<true, W, false, H> : dev::render_kernel_v3<false, W, false, H>;
+}
+
+template <int W, int H = dev::NODES_48>
+KernelFn v4_pick(bool count, bool tex) {
+    if (tex) return count ? dev::render_kernel_v4<true, W, true, H> : dev::render_kernel_v4<false, W, true, H>;
+    return count ? dev::render_kernel_v4<true, W, false, H> : dev::render_kernel_v4<false, W, false, H>;
 }
 
 KernelFn pick(int variant, bool count, bool tex) {
@@ -1185,13 +1407,59 @@ KernelFn pick(int variant, bool count, bool tex) {
     case 12: return count ? dev::render_kernel_v2<true, 6, 64> : dev::render_kernel_v2<false, 6, 64>;
     case 13: return v3_pick<1>(count, tex);
     case 14: return v3_pick<6>(count, tex);
-    default: return v3_pick<8>(count, tex);
+    case 15: return v3_pick<8>(count, tex);
+    case 16: return v4_pick<1>(count, tex);
+    case 17: return v4_pick<8>(count, tex);
+    case 18: return v3_pick<1, dev::NODES_HALF>(count, tex);
+    case 19: return v4_pick<1, dev::NODES_HALF>(count, tex);
+    case 20: return v4_pick<6, dev::NODES_HALF>(count, tex);
+    case 21: return v3_pick<1, dev::NODES_64>(count, tex);
+    default: return v4_pick<1, dev::NODES_64>(count, tex);
     }
 }
 
 thread_local int g_regen_threshold = 40;
+thread_local int g_persistent_waves = 0;  // 0: occupancy query
 
 constexpr size_t kLdsLimit = 160 * 1024;
+
+// Work-queue heads of the persistent kernel: a ring of counters per device, one slot per launch, zeroed
+// on the launch's stream right before it.  Slots are 64 B apart; a slot is reused only after
+// kQueueSlots further launches on that device, far more than can be in flight at once.
+constexpr uint32_t kQueueSlots = 4096;
+constexpr int kMaxDevices = 64;
+struct QueueRing {
+    uint32_t* buf = nullptr;
+    std::atomic<uint32_t> next{0};
+    int cus = 0;
+};
+QueueRing g_queues[kMaxDevices];
+std::mutex g_queue_mu;
+
+int acquire_queue(int device, uint32_t** head, int* cus) {
+    if (device < 0 || device >= kMaxDevices) {
+        set_error("rt_render: device ordinal out of range");
+        return RT_ERR_DEVICE;
+    }
+    QueueRing& q = g_queues[device];
+    {
+        std::lock_guard<std::mutex> lock(g_queue_mu);
+        if (!q.buf) {
+            void* p = nullptr;
+            int rc = hip_check(hipMalloc(&p, (size_t)kQueueSlots * 64), "rt_render: work queue allocation");
+            if (rc != RT_OK) return rc;
+            q.buf = (uint32_t*)p;
+            int n = 0;
+            rc = hip_check(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device),
+                           "rt_render: compute unit count");
+            if (rc != RT_OK) return rc;
+            q.cus = n;
+        }
+    }
+    *head = q.buf + (size_t)(q.next.fetch_add(1u) % kQueueSlots) * 16u;
+    *cus = q.cus;
+    return RT_OK;
+}
 
 }  // namespace
 
@@ -1235,6 +1503,15 @@ int rt_set_tuning(int key, int value) {
         g_leaf_max = value;
         return prev;
     }
+    if (key == RT_TUNE_PERSISTENT_WAVES) {
+        if (value < 0 || value > 16) {
+            set_error("rt_set_tuning: persistent waves per SIMD must be in [0, 16]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_persistent_waves;
+        g_persistent_waves = value;
+        return prev;
+    }
     set_error("rt_set_tuning: unknown key");
     return RT_ERR_INVALID_ARGUMENT;
 }
@@ -1268,6 +1545,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.nodes = (const float4*)S.nodes;
     P.nodes48 = (const float4*)S.nodes48;
     P.refs16 = (const uint32_t*)S.refs16;
+    P.nodes32 = (const uint32_t*)S.nodes32;
     P.prims = (const float4*)S.prims;
     P.mats = (const float4*)S.mats;
     P.imgs = (const int4*)S.imgs;
@@ -1336,6 +1614,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         variant = 13;
     if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
         variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
+    if (kVariants[variant].half && !S.has_half_nodes)  // a plane beyond the binary16 range: f32 boxes
+        variant = variant == 18 ? 13 : (variant == 19 ? 16 : 17);
+    if (kVariants[variant].persistent && (a->samples_per_pixel == 0 || a->max_depth == 0))
+        variant = kVariants[variant].half ? 18 : 13;  // the persistent kernel assumes every pixel traces a ray
     const Variant& V = kVariants[variant];
     // near-first traversal holds at most one deferred child per level below the root
     if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
@@ -1344,7 +1626,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
     size_t lds_bytes = (V.scene_lds ? scene_lds : 0) +
                        (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) +
-                       (V.stack == dev::STACK_LDS16 ? (size_t)dev::PK_WORDS * 64 * 4 + (size_t)(S.depth + 3) * 64 * 2 : 0);
+                       (V.stack == dev::STACK_LDS16
+                            ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::PK_WORDS) * 64 * 4 + (size_t)(S.depth + 3) * 64 * 2
+                            : 0);
     if (lds_bytes > kLdsLimit) {
         set_error("rt_render: scene does not fit in LDS for this variant");
         return RT_ERR_UNSUPPORTED;
@@ -1354,6 +1638,22 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.tiles_x = (a->width + tile - 1) / tile;
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
     hipStream_t s = (hipStream_t)stream;
+    uint32_t grid = tiles;
+    if (V.persistent) {
+        int device = 0, cus = 0, per_cu = 0;
+        int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
+        if (rc == RT_OK) rc = acquire_queue(device, &P.work_counter, &cus);
+        if (rc == RT_OK)
+            rc = hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, V.block, lds_bytes),
+                           "rt_render: occupancy query");
+        if (rc != RT_OK) return rc;
+        P.work_total = tiles * 64u;
+        if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
+        const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
+        grid = (uint32_t)(resident < tiles ? resident : tiles);
+        rc = hip_check(hipMemsetAsync(P.work_counter, 0, sizeof(uint32_t), s), "rt_render: work queue reset");
+        if (rc != RT_OK) return rc;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing) {
         (void)hipEventCreate(&e0);
@@ -1361,7 +1661,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         (void)hipEventRecord(e0, s);
     }
     (void)hipGetLastError();
-    hipLaunchKernelGGL(fn, dim3(tiles), dim3(V.block), lds_bytes, s, P);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(V.block), lds_bytes, s, P);
     int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
     if (g_timing) {
         (void)hipEventRecord(e1, s);

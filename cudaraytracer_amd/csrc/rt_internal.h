@@ -17,6 +17,7 @@
 //   mats    : 3 × float4 = 48 B per material:
 //               m0 = (bits(type | textype << 4), fuzz|ir, float(light_intensity), bits(image))
 //               m1 = (color.rgb, 0)   m2 = (color2.rgb, 0)
+//               dielectric: m1 = (1.0f / ir, r0², 0, 0) — the ir-only terms of Scatter, same binary32 ops
 //   images  : RGB8 texels of every image back to back; imgs[i] = (offset, width, height, 0) as int4
 //
 // Box padding: child boxes are the reference's primitive boxes (Hittable.cuh:112-116, 171-181, ...)
@@ -41,6 +42,8 @@ struct HostScene {
     std::vector<float> nodes;   // 16 floats per node
     std::vector<float> nodes48; // 12 floats per node: the three box float4 of `nodes` (v3 kernels)
     std::vector<uint32_t> refs16;  // per node: child 0 | child 1 << 16 as signed 16-bit references
+    std::vector<uint32_t> nodes32; // 8 words per node: binary16 child boxes + refs16 (HALF kernels)
+    bool has_half_nodes = false;   // every plane representable as a finite binary16 (rounded outward)
     std::vector<float> prims;   // 8 floats per primitive
     std::vector<float> mats;    // 12 floats per material
     std::vector<int32_t> imgs;  // 4 ints per image

@@ -51,6 +51,37 @@ RectGeom rect_geom(const rt_hittable_desc& h) {
     return g;
 }
 
+// binary16 helpers (host only, no _Float16 dependency).  Ordered key of a finite half: monotone in its
+// value (keys -0x7bff..0x7bff; +0 and -0 both map to 0).
+float half_value(int key) {
+    const uint32_t m = (uint32_t)(key < 0 ? -key : key);
+    const uint32_t e = m >> 10, f = m & 0x3ffu;
+    const float mag = e == 0 ? std::ldexp((float)f, -24) : std::ldexp((float)(1024u + f), (int)e - 25);
+    return key < 0 ? -mag : mag;
+}
+uint16_t half_bits(int key) { return key < 0 ? (uint16_t)(0x8000u | (uint32_t)(-key)) : (uint16_t)key; }
+
+// Largest finite binary16 <= v, as bits, or -1 if there is none (v < -65504 or NaN).
+int half_round_down(float v) {
+    if (!(v >= -65504.0f)) return -1;
+    int lo = -0x7bff, hi = 0x7bff;  // invariant: half_value(lo) <= v
+    while (lo < hi) {
+        const int mid = lo + (hi - lo + 1) / 2;
+        if (half_value(mid) <= v) lo = mid; else hi = mid - 1;
+    }
+    return half_bits(lo);
+}
+// Smallest finite binary16 >= v, as bits, or -1 if there is none.
+int half_round_up(float v) {
+    if (!(v <= 65504.0f)) return -1;
+    int lo = -0x7bff, hi = 0x7bff;  // invariant: half_value(hi) >= v
+    while (lo < hi) {
+        const int mid = lo + (hi - lo) / 2;
+        if (half_value(mid) >= v) hi = mid; else lo = mid + 1;
+    }
+    return half_bits(lo);
+}
+
 // Reference primitive box (Hittable.cuh:112-116, 171-181, 227-237, 283-293), grown outward.
 Box prim_box(const rt_hittable_desc& h) {
     Box b;
@@ -205,6 +236,17 @@ int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images
             o[4 + c] = m.albedo.color[c];
             o[8 + c] = m.albedo.color2[c];
         }
+        if (m.type == RT_DIELECTRIC) {
+            // ir-only terms of Dielectric::Scatter, with the kernel's binary32 operations (this file is
+            // compiled -ffp-contract=off): 1.0f / ir (Material.cuh:124) and Reflectance's r0² (:142-143)
+            volatile float ir = m.ir;
+            volatile float inv = 1.0f / ir;
+            volatile float r0 = (1.0f - ir) / (1.0f + ir);
+            volatile float r0sq = r0 * r0;
+            o[4] = inv;
+            o[5] = r0sq;
+            o[6] = 0.0f;
+        }
     }
     return RT_OK;
 }
@@ -291,6 +333,32 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         const Builder::Node& n = B.nodes[i];
         out->refs16[i] = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);  // valid when refs fit int16
     }
+    // binary16 child boxes (v3/v4 HALF kernels): planes rounded outward, so the box still contains the
+    // padded fp32 box and culling stays conservative; only when every plane is a finite binary16
+    out->has_half_nodes = true;
+    out->nodes32.assign((size_t)out->num_nodes * 8, 0u);
+    for (uint32_t i = 0; i < out->num_nodes && out->has_half_nodes; i++) {
+        const Builder::Node& n = B.nodes[i];
+        uint32_t* o = out->nodes32.data() + (size_t)i * 8;
+        uint16_t h[2][3][2];
+        for (int c = 0; c < 2; c++)
+            for (int a = 0; a < 3; a++) {
+                int lo = half_round_down(n.box[c].lo[a]), hi = half_round_up(n.box[c].hi[a]);
+                if (lo < 0 || hi < 0) {
+                    out->has_half_nodes = false;
+                    break;
+                }
+                h[c][a][0] = (uint16_t)lo;
+                h[c][a][1] = (uint16_t)hi;
+            }
+        if (!out->has_half_nodes) break;
+        auto pack = [](const uint16_t* lohi) { return (uint32_t)lohi[0] | ((uint32_t)lohi[1] << 16); };
+        o[0] = pack(h[0][0]); o[1] = pack(h[0][1]); o[2] = pack(h[1][0]); o[3] = pack(h[1][1]);
+        o[4] = pack(h[0][2]); o[5] = pack(h[1][2]);
+        o[6] = out->refs16[i];
+        o[7] = 0u;
+    }
+    if (!out->has_half_nodes) out->nodes32.clear();
     out->prims.resize((size_t)out->num_prims * 8);
     out->prim_source.resize(out->num_prims);
     for (uint32_t i = 0; i < out->num_prims; i++) {

@@ -255,7 +255,9 @@ int rt_set_variant(int variant);
  *   RT_TUNE_REGEN_THRESHOLD: resumable kernels leave traversal to shade/regenerate finished lanes when
  *   fewer than this many of a wave's 64 lanes are still tracing (1..64, default 40). */
 /*   RT_TUNE_LEAF_MAX: maximum primitives per BVH leaf used by later rt_scene_create calls (1..4, default 4). */
-enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1 };
+/*   RT_TUNE_PERSISTENT_WAVES: waves per SIMD of the persistent kernels' grid (0 = occupancy query, default;
+ *   1..16). */
+enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2 };
 int rt_set_tuning(int key, int value);
 
 /* Host-side helpers (no device needed). */
@@ -274,6 +276,14 @@ typedef struct rt_host_tables_info {
 } rt_host_tables_info;
 int rt_build_host_tables(const rt_scene_desc* desc, float* nodes, float* prims, float* materials,
                          int32_t* prim_source, rt_host_tables_info* info);
+
+/* The 32-B binary16 BVH nodes the HALF kernels read (8 words per node, same topology as `nodes` above):
+ *   w0..w1 = child 0 x/y planes, w2..w3 = child 1 x/y planes, w4 = child 0 z, w5 = child 1 z
+ *   (each word = lo | hi << 16 as binary16, lo rounded down and hi rounded up from the fp32 plane),
+ *   w6 = child 0 | child 1 << 16 (signed 16-bit references), w7 = 0.
+ * RT_ERR_UNSUPPORTED when a plane lies beyond the binary16 range (the kernels then use fp32 boxes).
+ * Size query with NULL nodes32.  Test/inspection helper; not part of the reference interface. */
+int rt_build_host_half_nodes(const rt_scene_desc* desc, uint32_t* nodes32, uint32_t* num_nodes);
 
 /* glibc random_r TYPE_3 restatement: rand() sequence after srand(seed) (RND macro, Math.cuh:12). */
 typedef struct rt_glibc_rand { int32_t r[34]; uint32_t idx; } rt_glibc_rand;

@@ -23,7 +23,9 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = list(range(16))
+VARIANTS = list(range(23))
+# v3 (13), persistent v4 (16), binary16 nodes (18), persistent + binary16 (19)
+KEY_VARIANTS = [13, 16, 18, 19]
 
 
 @pytest.fixture(autouse=True)
@@ -179,7 +181,9 @@ def test_material_update_without_rebuild():
     np.testing.assert_array_equal(r.image(), ref)
 
 
-def test_edge_cases_spp0_depth0_empty_and_inactive():
+@pytest.mark.parametrize("variant", KEY_VARIANTS)
+def test_edge_cases_spp0_depth0_empty_and_inactive(variant):
+    lib().rt_set_variant(variant)
     cfg = scenes.CONFIGS["c2"].scaled(48, 32, 3)
     sc = scenes.builtin(cfg.scene)
     ds = DeviceScene(sc)
@@ -223,7 +227,9 @@ def test_edge_cases_spp0_depth0_empty_and_inactive():
     assert int(r3.counters[0]) == cnt.rays == cfg.width * cfg.height * cfg.spp
 
 
-def test_single_primitive_scene():
+@pytest.mark.parametrize("variant", KEY_VARIANTS)
+def test_single_primitive_scene(variant):
+    lib().rt_set_variant(variant)
     cfg = scenes.CONFIGS["c1"].scaled(64, 36, 4)
     sc = scenes.builtin(cfg.scene)
     sc.hittables[0].is_active = 0
@@ -239,7 +245,9 @@ def test_single_primitive_scene():
     np.testing.assert_array_equal(r.image(), ref)
 
 
-def test_accumulate_first_frame_equals_plain_frame():
+@pytest.mark.parametrize("variant", KEY_VARIANTS)
+def test_accumulate_first_frame_equals_plain_frame(variant):
+    lib().rt_set_variant(variant)
     case = CASE_BY_NAME["c5_textured_160x96_s4"]
     cfg = case.cfg()
     g = load_golden(case.name)
@@ -329,3 +337,21 @@ def test_full_size_c2_determinism_and_frame_sequence():
     c = r.image()
     s = image_stats(b, c)
     assert s["exact"] < 0.9 and abs(s["mean_signed"]) < 0.5  # new noise, same expectation
+
+
+@pytest.mark.parametrize("variant", KEY_VARIANTS)
+def test_scene_beyond_binary16_range_matches_oracle(variant):
+    """A plane beyond ±65504 cannot be a binary16 node: the HALF variants fall back to fp32 boxes."""
+    cfg = scenes.CONFIGS["c1"].scaled(64, 36, 4)
+    sc = scenes.builtin(cfg.scene)
+    sc.hittables[0].center[0] = 70000.0
+    lib().rt_set_variant(variant)
+    ds = DeviceScene(sc)
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
+    np.testing.assert_array_equal(r.image(), ref)
+    assert int(r.counters[0]) == cnt.rays

@@ -13,6 +13,7 @@ ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--spp", type=int, default=0)
 ap.add_argument("--thresholds", default="40", help="regen thresholds to try for resumable variants (>= 8)")
 ap.add_argument("--leafmax", default="4", help="BVH leaf sizes to try (RT_TUNE_LEAF_MAX)")
+ap.add_argument("--pwaves", default="0", help="persistent grid waves/SIMD to try (RT_TUNE_PERSISTENT_WAVES)")
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 if args.spp:
@@ -21,7 +22,8 @@ variants = []
 for lm in (int(x) for x in args.leafmax.split(",")):
     for v in (int(v) for v in args.variants.split(",")):
         for th in ([int(t) for t in args.thresholds.split(",")] if v >= 8 else [40]):
-            variants.append((v, th, lm))
+            for pw in ([int(p) for p in args.pwaves.split(",")] if v in (16, 17, 19, 20) else [0]):
+                variants.append((v, th, lm, pw))
 scenes_by_lm = {}
 for lm in sorted({v[2] for v in variants}):
     lib().rt_set_tuning(1, lm)
@@ -32,15 +34,17 @@ r.render_init()
 inp = cfg.inputs()
 times = {v: [] for v in variants}
 rays = {}
-for v, th, lm in variants:  # warm-up / JIT of each variant
+for v, th, lm, pw in variants:  # warm-up / JIT of each variant
     lib().rt_set_variant(v)
     lib().rt_set_tuning(0, th)
+    lib().rt_set_tuning(2, pw)
     r.render(scenes_by_lm[lm], cfg.spp, cfg.depth, inp)
 torch.cuda.synchronize()
 for rnd in range(args.rounds):
     for v in variants:
         lib().rt_set_variant(v[0])
         lib().rt_set_tuning(0, v[1])
+        lib().rt_set_tuning(2, v[3])
         r.counters.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -51,4 +55,4 @@ for rnd in range(args.rounds):
         rays[v] = int(r.counters[0])
 for v in variants:
     med = statistics.median(times[v])
-    print(f"{args.config} variant {v[0]} thr {v[1]} leafmax {v[2]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)
+    print(f"{args.config} variant {v[0]} thr {v[1]} leafmax {v[2]} pwaves {v[3]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)

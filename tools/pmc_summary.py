@@ -22,6 +22,12 @@ der = {
     "hbm_read_bytes(FETCH_SIZE*1024*2, gfx950 1/2 correction)": g("FETCH_SIZE") * 1024 * 2,
     "hbm_write_bytes(WRITE_SIZE*1024)": g("WRITE_SIZE") * 1024,
     "kernel_clock_ghz_est": None,
+    "vmem_latency_cycles": g("SQ_INST_LEVEL_VMEM") / g("SQ_INSTS_VMEM"),
+    "lds_latency_cycles": g("SQ_INST_LEVEL_LDS") / g("SQ_INSTS_LDS"),
+    "icache_miss_per_ifetch": g("SQC_ICACHE_MISSES") / g("SQ_IFETCH"),
+    "ta_addr_fifo_full_frac": g("SQ_VMEM_TA_ADDR_FIFO_FULL") / 256 / xcd_cycles,
+    "ta_cmd_fifo_full_frac": g("SQ_VMEM_TA_CMD_FIFO_FULL") / 256 / xcd_cycles,
+    "valu_trans_frac": g("SQ_INSTS_VALU_TRANS_F32") / g("SQ_INSTS_VALU"),
 }
 out = {"kernel": meta, "derived": der, "counters": vals}
 print(json.dumps(out, indent=1))
