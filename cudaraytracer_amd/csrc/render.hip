@@ -1203,6 +1203,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     Cursor c{kSentinel16, 0, -1, 0u, FLT_MAX, MODE_NEED};
     uint32_t wq_next = 0u, wq_end = 0u;  // wave-uniform: the wave's current chunk of work indices
     bool drained = false;                // wave-uniform: the frame's queue is empty
+    uint32_t wave_pixels = 0u;           // wave-uniform: pixels this wave has taken
     const uint32_t threshold = P.regen_threshold;
 
     while (true) {
@@ -1265,13 +1266,14 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
                         rng = load_rng(P.state + (size_t)pix * 12);
                         col = mk(0.0f, 0.0f, 0.0f);
                         sample = 0u;
-                        cnt.primary += P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
                         cam = true;
                     }
                 }
                 const uint32_t taken = min((uint32_t)__popcll(needm), avail);
                 wq_next += taken;
-                needm = __ballot(need);
+                const uint64_t still = __ballot(need);
+                wave_pixels += (uint32_t)__popcll(needm & ~still);
+                needm = still;
             }
             if (need) c.mode = MODE_DONE;
         }
@@ -1287,6 +1289,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
         if (__ballot(c.mode != MODE_DONE) == 0) break;
     }
     cnt.rays = park[PK_RAYS * 64];
+    // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
+    cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
@@ -1370,6 +1374,7 @@ constexpr Variant kVariants[] = {
     {false, dev::STACK_LDS16, 1, 0, true, 64, false, true}, {false, dev::STACK_LDS16, 1, 0, true, 64, true, true},
     {false, dev::STACK_LDS16, 6, 0, true, 64, true, true},
     {false, dev::STACK_LDS16, 1, 0, true, 64}, {false, dev::STACK_LDS16, 1, 0, true, 64, true},
+    {false, dev::STACK_LDS16, 7, 0, true, 64, true},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -1414,7 +1419,8 @@ KernelFn pick(int variant, bool count, bool tex) {
     case 19: return v4_pick<1, dev::NODES_HALF>(count, tex);
     case 20: return v4_pick<6, dev::NODES_HALF>(count, tex);
     case 21: return v3_pick<1, dev::NODES_64>(count, tex);
-    default: return v4_pick<1, dev::NODES_64>(count, tex);
+    case 22: return v4_pick<1, dev::NODES_64>(count, tex);
+    default: return v4_pick<7, dev::NODES_64>(count, tex);
     }
 }
 
@@ -1610,8 +1616,11 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
     const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
     int variant = g_variant;
-    if (variant < 0 || variant >= kNumVariants)  // auto: fastest measured (profiles/r01_ab_*): v3
-        variant = 13;
+    // auto: the fastest measured kernel per workload shape (profiles/r01_*): the persistent v4 for short
+    // or deep paths per pixel (config 5: 1 spp, 0.54 vs 0.80 ms; config 3: depth 16, 438 vs 461 ms), v3
+    // for the many-sample frames (config 2: 64 spp, 26.1 vs 27.4 ms)
+    if (variant < 0 || variant >= kNumVariants)
+        variant = (a->samples_per_pixel < 32 || a->max_depth > 8) ? 22 : 13;
     if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
         variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
     if (kVariants[variant].half && !S.has_half_nodes)  // a plane beyond the binary16 range: f32 boxes
