@@ -62,6 +62,26 @@ def cpu_baseline(cfg: scenes.Config, target_s: float) -> dict:
                       f"frame at {cfg.spp} spp, depth {cfg.depth}: {rays} rays in {dt:.2f} s, {threads} OpenMP threads"}
 
 
+def philox_mode(cfg: scenes.Config, scene: DeviceScene, inputs, steps: int) -> dict:
+    """Secondary figure: the same frames with the stateless Philox RNG (RT_FLAG_RNG_PHILOX, no per-pixel
+    RNG state in HBM).  Not the headline: the reference's stream is XORWOW."""
+    r = Renderer(cfg.width, cfg.height, rng="philox")
+    r.render_init()
+    r.render(scene, cfg.spp, cfg.depth, inputs)  # warm-up
+    torch.cuda.synchronize()
+    r.counters.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        r.render(scene, cfg.spp, cfg.depth, inputs)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    rays = int(r.counters[0]) / steps
+    return {"value": round(rays / ms / 1e3, 2), "unit": "Mray/s", "kernel_ms": round(ms, 3),
+            "rays_per_frame": int(rays), "hbm_rng_state_bytes": 0}
+
+
 def pmc_traffic(config: str, n_gpus: int):
     """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}_n{n_gpus}.json")
@@ -78,8 +98,12 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--variant", type=int, default=-1, help="kernel variant (rt_set_variant); -1 = automatic")
+    ap.add_argument("--rng", choices=("xorwow", "philox"), default="xorwow",
+                    help="xorwow: the reference's per-pixel cuRAND state (parity mode, headline); philox: stateless "
+                         "Philox4x32-10 streams (RT_FLAG_RNG_PHILOX)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-philox-line", action="store_true", help="skip the secondary Philox-mode timing (N=1)")
     args = ap.parse_args()
 
     rank, world, local_rank = parallel.env_rank()
@@ -96,7 +120,7 @@ def main() -> None:
     lib().rt_set_variant(args.variant)
 
     band = parallel.DEFAULT_BAND_ROWS if world > 1 else cfg.height
-    r = Renderer(cfg.width, cfg.height, device=local_rank, band_rows=band, num_ranks=world, rank=rank)
+    r = Renderer(cfg.width, cfg.height, device=local_rank, band_rows=band, num_ranks=world, rank=rank, rng=args.rng)
     scene = DeviceScene(scenes.builtin(cfg.scene))
     inputs = cfg.inputs()
     r.render_init()
@@ -160,6 +184,7 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "rng": args.rng,
             "data": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
             "config": {
                 "workload": (f"{args.config}: {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}, "
@@ -184,6 +209,8 @@ def main() -> None:
                 "prim_tests_per_ray": round(c[2] / max(1, c[0]), 2),
             },
         }
+        if world == 1 and args.rng == "xorwow" and not args.no_philox_line:
+            line["philox_mode"] = philox_mode(cfg, scene, inputs, args.steps)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(line), flush=True)

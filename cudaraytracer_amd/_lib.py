@@ -10,6 +10,8 @@ import os
 from . import abi
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_hip.so")
+# A/B experiments only: RT_HIP_LIB names another in-tree build of the same library (tools/ab_builds.sh).
+LIB_PATH = os.environ.get("RT_HIP_LIB", LIB_PATH)
 
 # Every symbol include/rt_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = [

@@ -19,6 +19,7 @@ RT_FLAG_NO_STATE_WRITEBACK = 1 << 1
 RT_FLAG_ACCUMULATE = 1 << 2
 RT_FLAG_RIUS_LEFT_TO_RIGHT = 1 << 3
 RT_FLAG_COUNT_TESTS = 1 << 4
+RT_FLAG_RNG_PHILOX = 1 << 5
 
 STATUS = {
     0: "RT_OK",
@@ -132,6 +133,9 @@ class RenderArgs(C.Structure):
         ("reserved", C.c_uint32),
         ("tiling", Tiling),
         ("inputs", InputStruct),
+        ("rng_seed", C.c_uint64),
+        ("rng_frame", C.c_uint32),
+        ("reserved2", C.c_uint32),
     ]
 
 

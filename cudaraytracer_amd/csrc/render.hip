@@ -27,6 +27,7 @@
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 
 #include "rt_internal.h"
 #include "rt_scene_device.h"
@@ -41,6 +42,7 @@ struct f3 {
     float x, y, z;
 };
 typedef __fp16 half2v __attribute__((ext_vector_type(2)));
+typedef float fl2 __attribute__((ext_vector_type(2)));
 
 // BVH node layouts read by the v3/v4 traversal (template argument NODES)
 enum NodeLayout { NODES_48 = 0, NODES_HALF = 1, NODES_64 = 2 };
@@ -82,12 +84,25 @@ __device__ __forceinline__ float uniform(Rng& s) {
 
 // RandomInUnitSphere (Math.cuh:252-260) with Random() (Math.cuh:231-234).  rtl: the components of
 // Vec3(ξa, ξb, ξc) are filled right to left (z = first draw), as the survey's g++ build evaluated it.
-__device__ __forceinline__ f3 random_in_unit_sphere(Rng& s, bool rtl) {
+// Groups of consecutive draws (same values, same order as that many uniform() calls).  For the XORWOW
+// state these are plain sequences; the Philox engine overloads them so a group generates at most one new
+// block of four words (one generation site per group instead of one per draw).
+template <class R> __device__ __forceinline__ void draw2(R& s, float& a, float& b) {
+    a = uniform(s);
+    b = uniform(s);
+}
+template <class R> __device__ __forceinline__ void draw3(R& s, float& a, float& b, float& c) {
+    a = uniform(s);
+    b = uniform(s);
+    c = uniform(s);
+}
+
+template <class R>
+__device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
     f3 p;
     do {
-        float a = uniform(s);
-        float b = uniform(s);
-        float c = uniform(s);
+        float a, b, c;
+        draw3(s, a, b, c);
         f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
         p = sub(scale(2.0f, r), mk(1.0f, 1.0f, 1.0f));
     } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
@@ -127,6 +142,8 @@ struct KParams {
     uint32_t regen_threshold;  // v2: lanes still tracing below which finished lanes are regenerated
     uint32_t* work_counter;    // v4: the frame's work queue head (zeroed before the launch)
     uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
+    uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
+    uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
 };
 
 constexpr int kStackMax = 64;
@@ -345,10 +362,12 @@ struct Camera {
 };
 
 // Camera ray of one sample (Kernel.cu:139-146): two uniforms, then the reference's plane construction.
-template <class PP>
-__device__ __forceinline__ void camera_ray(PP P, const Camera& cam, Rng& rng, f3& ro, f3& rd) {
-    const float u = (cam.xf + uniform(rng)) / P->width_f;
-    const float v = (cam.yf + uniform(rng)) / P->width_f;
+template <class PP, class R>
+__device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& ro, f3& rd) {
+    float xi1, xi2;
+    draw2(rng, xi1, xi2);
+    const float u = (cam.xf + xi1) / P->width_f;
+    const float v = (cam.yf + xi2) / P->width_f;
     const f3 dist = add(scale(u, cam.right), scale(v, cam.up));
     const f3 start = add(add(scale(P->near_plane, dist), cam.origin), cam.fov_fwd);
     const f3 second = add(add(scale(P->far_plane, dist), cam.k10_fwd), cam.origin);
@@ -359,9 +378,9 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, Rng& rng, f3
 // One iteration of color()'s bounce loop after the closest-hit query (Kernel.cu:40-76): sky on a miss,
 // emission, or Scatter of the hit material.  Returns true when the path ended (contribution in `contrib`,
 // `emitted * cur_attenuation` or `cur_attenuation * sky`); false when it continues with (ro, rd, att).
-template <bool TEX = true, class PP>
+template <bool TEX = true, class PP, class R>
 __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, int hit, float t, f3& ro,
-                                      f3& rd, f3& att, Rng& rng, bool rtl, f3& contrib) {
+                                      f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
     // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
     uint32_t mtype = 0xffu;  // 0xff: miss
@@ -489,11 +508,16 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
 }
 
 // Pixel epilogue (Kernel.cu:149-157): RNG state store, average, gamma 2, RGBA8 pack; optional outputs.
-__device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32_t* st, const Rng& rng, f3 col) {
+__device__ __forceinline__ void store_rng(const KParams& P, uint32_t* st, const Rng& rng) {
     if (!(P.flags & RT_FLAG_NO_STATE_WRITEBACK)) {
         *reinterpret_cast<uint4*>(st) = make_uint4(rng.d, rng.v0, rng.v1, rng.v2);
         *reinterpret_cast<uint2*>(st + 4) = make_uint2(rng.v3, rng.v4);
     }
+}
+
+template <class R>
+__device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32_t* st, const R& rng, f3 col) {
+    store_rng(P, st, rng);
     f3 c;
     if (P.flags & RT_FLAG_ACCUMULATE) {
         float4 a = P.accum[pix];
@@ -525,8 +549,8 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt
     }
 }
 
-template <bool COUNT_TESTS>
-__device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint32_t* st, const Rng& rng, f3 col,
+template <bool COUNT_TESTS, class R>
+__device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint32_t* st, const R& rng, f3 col,
                                              const Counts& cnt) {
     write_pixel(P, pix, st, rng, col);
     flush_counts<COUNT_TESTS>(P, cnt);
@@ -536,9 +560,10 @@ __device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint3
 // ceil(W/16)); BLOCK = 64: one wave per workgroup covering an 8×8 tile (P.tiles_x = ceil(W/8)).  Returns
 // false for lanes outside the (local) image or outside the faithful floor-division grid (Kernel.cu:184).
 template <int BLOCK = kBlock>
-__device__ __forceinline__ bool lane_pixel(const KParams& P, uint32_t& x, uint32_t& g, size_t& pix) {
+__device__ __forceinline__ bool lane_pixel(const KParams& P, uint32_t& x, uint32_t& g, size_t& pix,
+                                           uint32_t tile = blockIdx.x) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t bx = blockIdx.x % P.tiles_x, by = blockIdx.x / P.tiles_x;
+    const uint32_t bx = tile % P.tiles_x, by = tile / P.tiles_x;
     uint32_t ly;
     if constexpr (BLOCK == 64) {
         x = bx * 8 + (lane & 7u);
@@ -582,6 +607,93 @@ __device__ __forceinline__ Rng load_rng(const uint32_t* st) {
     const uint4 s03 = *reinterpret_cast<const uint4*>(st);
     const uint2 s45 = *reinterpret_cast<const uint2*>(st + 4);
     return Rng{s03.x, s03.y, s03.z, s03.w, s45.x, s45.y};
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Perf-mode RNG (RT_FLAG_RNG_PHILOX): hipRAND/rocRAND Philox4x32-10 (rocrand_philox4x32_10.h:270-303,
+// rocrand_uniform.h:65-68, 239-242).  The pixel's stream is rocrand_init(seed, subsequence = global pixel
+// index, offset = frame << 34): draw n of the frame is word n & 3 of philox10(ctr = {n >> 2, frame,
+// pixel, 0}, key = seed), generated four at a time.  Nothing per pixel lives in HBM: the lane holds the
+// draw index, the current block of four words and the pixel index (six words, as the XORWOW state);
+// key and frame are launch-uniform kernel arguments.
+// ---------------------------------------------------------------------------------------------------
+struct RngPhilox {
+    uint32_t n, r0, r1, r2, r3, pix;
+};
+
+// Block `blk` of the lane's stream: philox10(ctr = {blk, frame, pixel, 0}, key = seed) into s.r0..r3.
+__device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
+    KParamsC* q = kparams_reload();
+    uint32_t c0 = blk, c1 = q->rng_frame, c2 = s.pix, c3 = 0u;
+    uint32_t k0 = q->rng_key_lo, k1 = q->rng_key_hi;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {  // single_round + bumpkey (rocrand_philox4x32_10.h:286-303)
+        const uint64_t m0 = (uint64_t)0xD2511F53u * c0;  // one v_mad_u64_u32 for lo and hi
+        const uint64_t m1 = (uint64_t)0xCD9E8D57u * c2;
+        c0 = (uint32_t)(m1 >> 32) ^ c1 ^ k0;
+        c1 = (uint32_t)m1;
+        c2 = (uint32_t)(m0 >> 32) ^ c3 ^ k1;
+        c3 = (uint32_t)m0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    s.r0 = c0;
+    s.r1 = c1;
+    s.r2 = c2;
+    s.r3 = c3;
+}
+
+__device__ __forceinline__ float philox_to_uniform(uint32_t x) {
+    return 2.3283064e-10f + (float)x * 2.3283064e-10f;  // 2^-32 + x·2^-32 (exact product)
+}
+
+// Word j (0..3) of the current block.
+__device__ __forceinline__ uint32_t philox_word(const RngPhilox& s, uint32_t j) {
+    return j < 2u ? (j == 0u ? s.r0 : s.r1) : (j == 2u ? s.r2 : s.r3);
+}
+
+__device__ __forceinline__ float uniform(RngPhilox& s) {
+    if ((s.n & 3u) == 0u) philox_block(s, s.n >> 2);
+    const float u = philox_to_uniform(philox_word(s, s.n & 3u));
+    s.n++;
+    return u;
+}
+
+// k (2 or 3) consecutive draws with at most one block generation: the words left in the current block
+// (none when n is a multiple of 4) come first, then the next block.
+template <int K>
+__device__ __forceinline__ void philox_group(RngPhilox& s, uint32_t* out) {
+    const uint32_t j = s.n & 3u;
+    const uint32_t left = j == 0u ? 0u : 4u - j;  // unused words of the current block
+    uint32_t old[3];
+#pragma unroll
+    for (int i = 0; i < K; i++) old[i] = philox_word(s, (j + (uint32_t)i) & 3u);
+    if (left < (uint32_t)K) philox_block(s, (s.n + left) >> 2);
+#pragma unroll
+    for (int i = 0; i < K; i++) out[i] = (uint32_t)i < left ? old[i] : philox_word(s, (uint32_t)i - left);
+    s.n += (uint32_t)K;
+}
+__device__ __forceinline__ void draw2(RngPhilox& s, float& a, float& b) {
+    uint32_t w[2];
+    philox_group<2>(s, w);
+    a = philox_to_uniform(w[0]);
+    b = philox_to_uniform(w[1]);
+}
+__device__ __forceinline__ void draw3(RngPhilox& s, float& a, float& b, float& c) {
+    uint32_t w[3];
+    philox_group<3>(s, w);
+    a = philox_to_uniform(w[0]);
+    b = philox_to_uniform(w[1]);
+    c = philox_to_uniform(w[2]);
+}
+
+__device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPhilox&) {}  // stateless in HBM
+
+// Start of a pixel's frame: its XORWOW state from HBM, or its Philox stream at draw 0.
+template <class R> __device__ __forceinline__ R begin_rng(const uint32_t* st, uint32_t pixel);
+template <> __device__ __forceinline__ Rng begin_rng<Rng>(const uint32_t* st, uint32_t) { return load_rng(st); }
+template <> __device__ __forceinline__ RngPhilox begin_rng<RngPhilox>(const uint32_t*, uint32_t pixel) {
+    return RngPhilox{0u, 0u, 0u, 0u, 0u, pixel};
 }
 
 // Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop: every
@@ -883,7 +995,8 @@ __device__ __forceinline__ void v3_start_trace(uint32_t num_nodes, Cursor& c, ui
 }
 
 // A path ended with `contrib`: accumulate (Kernel.cu:147), then the next sample's camera ray, or finish.
-__device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uint32_t g, f3 contrib, Rng& rng,
+template <class R>
+__device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uint32_t g, f3 contrib, R& rng,
                                                f3& col, f3& att, uint32_t& sample, uint32_t& depth, f3& ro,
                                                f3& rd, Cursor& c, uint32_t& rays) {
     col = add(col, contrib);
@@ -902,15 +1015,37 @@ __device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uin
     c.mode = MODE_DONE;
 }
 
-__device__ __forceinline__ void v3_park(uint32_t* park, const Rng& rng, f3 col, f3 att, uint32_t sample,
+// The six RNG words of a lane: XORWOW d, v[5]; Philox draw index, block of four words, pixel index.
+__device__ __forceinline__ void park_rng(uint32_t* park, const Rng& r) {
+    park[(PK_RNG + 0) * 64] = r.d;
+    park[(PK_RNG + 1) * 64] = r.v0;
+    park[(PK_RNG + 2) * 64] = r.v1;
+    park[(PK_RNG + 3) * 64] = r.v2;
+    park[(PK_RNG + 4) * 64] = r.v3;
+    park[(PK_RNG + 5) * 64] = r.v4;
+}
+__device__ __forceinline__ void park_rng(uint32_t* park, const RngPhilox& r) {
+    park[(PK_RNG + 0) * 64] = r.n;
+    park[(PK_RNG + 1) * 64] = r.r0;
+    park[(PK_RNG + 2) * 64] = r.r1;
+    park[(PK_RNG + 3) * 64] = r.r2;
+    park[(PK_RNG + 4) * 64] = r.r3;
+    park[(PK_RNG + 5) * 64] = r.pix;
+}
+__device__ __forceinline__ void unpark_rng(const uint32_t* park, Rng& r) {
+    r = Rng{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
+            park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
+}
+__device__ __forceinline__ void unpark_rng(const uint32_t* park, RngPhilox& r) {
+    r = RngPhilox{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
+                  park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
+}
+
+template <class R>
+__device__ __forceinline__ void v3_park(uint32_t* park, const R& rng, f3 col, f3 att, uint32_t sample,
                                         uint32_t depth, uint32_t rays) {
     park[PK_RAYS * 64] = rays;
-    park[(PK_RNG + 0) * 64] = rng.d;
-    park[(PK_RNG + 1) * 64] = rng.v0;
-    park[(PK_RNG + 2) * 64] = rng.v1;
-    park[(PK_RNG + 3) * 64] = rng.v2;
-    park[(PK_RNG + 4) * 64] = rng.v3;
-    park[(PK_RNG + 5) * 64] = rng.v4;
+    park_rng(park, rng);
     park[(PK_COL + 0) * 64] = __float_as_uint(col.x);
     park[(PK_COL + 1) * 64] = __float_as_uint(col.y);
     park[(PK_COL + 2) * 64] = __float_as_uint(col.z);
@@ -921,11 +1056,11 @@ __device__ __forceinline__ void v3_park(uint32_t* park, const Rng& rng, f3 col, 
     park[PK_DEPTH * 64] = depth;
 }
 
-__device__ __forceinline__ void v3_unpark(const uint32_t* park, Rng& rng, f3& col, f3& att, uint32_t& sample,
+template <class R>
+__device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col, f3& att, uint32_t& sample,
                                           uint32_t& depth, uint32_t& rays) {
     rays = park[PK_RAYS * 64];
-    rng = Rng{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
-              park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
+    unpark_rng(park, rng);
     col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
              __uint_as_float(park[(PK_COL + 2) * 64]));
     att = mk(__uint_as_float(park[(PK_ATT + 0) * 64]), __uint_as_float(park[(PK_ATT + 1) * 64]),
@@ -977,7 +1112,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 ch0 = (int)r2.x;
                 ch1 = (int)r2.y;
             } else {  // 48 B of f32 boxes + 4 B of references
-                const uint32_t noff = (uint32_t)node * 48u;
+                uint32_t noff;  // node · 48 with the full-rate 24-bit multiply (LLVM otherwise emits v_mul_lo_u32)
+                asm("v_mul_u32_u24 %0, 48, %1" : "=v"(noff) : "v"(node));
                 n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
                 n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
                 n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
@@ -1081,11 +1217,20 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     if (c.node == kSentinel16 && c.leaf == 0) c.mode = MODE_SHADE;
 }
 
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48>
-__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
+// LDS slice of this wave: WPG independent waves share a workgroup (no barriers), each with its own
+// P.lds_wave_words words of parked state + stack.
+__device__ __forceinline__ uint32_t* wave_lds(float4* lds, const KParams& P) {
+    return (uint32_t*)lds + (threadIdx.x >> 6) * P.lds_wave_words;
+}
+
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48, int WPG = 1, bool PHILOX = false>
+__global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
+    using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     extern __shared__ float4 lds[];
-    uint32_t* const park = (uint32_t*)lds + threadIdx.x;                                 // word k: park[k * 64]
-    int16_t* const stk = reinterpret_cast<int16_t*>((uint32_t*)lds + PK_WORDS * 64) + threadIdx.x;  // stk[j * 64]
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t* const wl = wave_lds(lds, P);
+    uint32_t* const park = wl + lane;                                                  // word k: park[k * 64]
+    int16_t* const stk = reinterpret_cast<int16_t*>(wl + PK_WORDS * 64) + lane;        // stk[j * 64]
     // node boxes and packed child references through buffer descriptors: 32-bit offsets, no 64-bit
     // address arithmetic per visit; 48 B of boxes + 4 B of references per node
     const __amdgpu_buffer_rsrc_t nrsrc =
@@ -1097,7 +1242,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     const float4* __restrict__ prims = P.prims;
     uint32_t x, g;
     size_t pix;
-    if (!lane_pixel<64>(P, x, g, pix)) return;
+    if (!lane_pixel<64>(P, x, g, pix, blockIdx.x * WPG + (threadIdx.x >> 6))) return;
     const bool rtl = P.rius_rtl != 0;
     stk[0] = (int16_t)kSentinel16;  // two sentinel pads below the stack: popping an empty stack yields
     stk[64] = (int16_t)kSentinel16;  // kSentinel16 without a bounds test
@@ -1108,7 +1253,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
 
     {  // first camera ray of the pixel
         uint32_t* st = P.state + pix * 12;
-        Rng rng = load_rng(st);
+        R rng = begin_rng<R>(st, g * P.width + x);  // global pixel index (Kernel.cu:119)
         f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
         uint32_t sample = (uint32_t)-1, depth = 0, rays = 0;
         if (P.spp > 0) v3_next_sample(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
@@ -1121,7 +1266,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, prims, stk, threshold, ro, rd, c, cnt);
         }
         if (c.mode == MODE_SHADE) {
-            Rng rng;
+            R rng;
             f3 col, att;
             uint32_t sample, depth, rays;
             v3_unpark(park, rng, col, att, sample, depth, rays);
@@ -1141,7 +1286,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         }
         if (__ballot(c.mode != MODE_DONE) == 0) break;
     }
-    Rng rng;
+    R rng;
     f3 col, att;
     uint32_t sample, depth, rays;
     v3_unpark(park, rng, col, att, sample, depth, rays);
@@ -1181,11 +1326,14 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
     return true;
 }
 
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48>
-__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48, int WPG = 1, bool PHILOX = false>
+__global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
+    using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     extern __shared__ float4 lds[];
-    uint32_t* const park = (uint32_t*)lds + threadIdx.x;
-    int16_t* const stk = reinterpret_cast<int16_t*>((uint32_t*)lds + PK_WORDS4 * 64) + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t* const wl = wave_lds(lds, P);
+    uint32_t* const park = wl + lane;
+    int16_t* const stk = reinterpret_cast<int16_t*>(wl + PK_WORDS4 * 64) + lane;
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_HALF ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes32, (short)0, (int)(P.num_nodes * 32u), 0x00020000)
         : NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
@@ -1208,7 +1356,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
 
     while (true) {
         if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, prims, stk, threshold, ro, rd, c, cnt);
-        Rng rng;
+        R rng;
         f3 col, att;
         uint32_t sample, depth, rays;
         bool cam = false, fin = false;
@@ -1263,7 +1411,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
                         park[PK_X * 64] = x;
                         park[PK_G * 64] = g;
                         park[PK_PIX * 64] = pix;
-                        rng = load_rng(P.state + (size_t)pix * 12);
+                        rng = begin_rng<R>(P.state + (size_t)pix * 12, g * P.width + x);
                         col = mk(0.0f, 0.0f, 0.0f);
                         sample = 0u;
                         cam = true;
@@ -1358,6 +1506,7 @@ struct Variant {
     int block;      // threads per workgroup
     bool persistent = false;  // render_kernel_v4: device-filling grid + work queue
     bool half = false;        // binary16 child boxes (32-B nodes)
+    int wpg = 1;              // v3/v4: independent waves per workgroup (block = 64 · wpg)
 };
 
 // rt_set_variant(i) selects kVariants[i]
@@ -1375,6 +1524,9 @@ constexpr Variant kVariants[] = {
     {false, dev::STACK_LDS16, 6, 0, true, 64, true, true},
     {false, dev::STACK_LDS16, 1, 0, true, 64}, {false, dev::STACK_LDS16, 1, 0, true, 64, true},
     {false, dev::STACK_LDS16, 7, 0, true, 64, true},
+    // 24..27: v3 / v4 (64-B nodes) with 2 or 4 independent waves per workgroup
+    {false, dev::STACK_LDS16, 1, 0, true, 128, false, false, 2}, {false, dev::STACK_LDS16, 1, 0, true, 256, false, false, 4},
+    {false, dev::STACK_LDS16, 1, 0, true, 128, true, false, 2},  {false, dev::STACK_LDS16, 1, 0, true, 256, true, false, 4},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -1383,19 +1535,34 @@ KernelFn pick_count(bool count) {
     return count ? dev::render_kernel<L, S, true, W> : dev::render_kernel<L, S, false, W>;
 }
 
-template <int W, int H = dev::NODES_48>
+template <int W, int H = dev::NODES_48, int G = 1, bool PH = false>
 KernelFn v3_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v3<true, W, true, H> : dev::render_kernel_v3<false, W, true, H>;
-    return count ? dev::render_kernel_v3<true, W, false, H> : dev::render_kernel_v3<false, W, false, H>;
+    if (tex) return count ? dev::render_kernel_v3<true, W, true, H, G, PH> : dev::render_kernel_v3<false, W, true, H, G, PH>;
+    return count ? dev::render_kernel_v3<true, W, false, H, G, PH> : dev::render_kernel_v3<false, W, false, H, G, PH>;
 }
 
-template <int W, int H = dev::NODES_48>
+template <int W, int H = dev::NODES_48, int G = 1, bool PH = false>
 KernelFn v4_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v4<true, W, true, H> : dev::render_kernel_v4<false, W, true, H>;
-    return count ? dev::render_kernel_v4<true, W, false, H> : dev::render_kernel_v4<false, W, false, H>;
+    if (tex) return count ? dev::render_kernel_v4<true, W, true, H, G, PH> : dev::render_kernel_v4<false, W, true, H, G, PH>;
+    return count ? dev::render_kernel_v4<true, W, false, H, G, PH> : dev::render_kernel_v4<false, W, false, H, G, PH>;
 }
 
-KernelFn pick(int variant, bool count, bool tex) {
+// Kernels with the Philox engine (RT_FLAG_RNG_PHILOX): the v3/v4 variants the automatic choice uses.
+constexpr int kPhiloxVariants[] = {13, 22, 25};
+bool philox_capable(int variant) {
+    for (int v : kPhiloxVariants)
+        if (v == variant) return true;
+    return false;
+}
+
+KernelFn pick(int variant, bool count, bool tex, bool philox) {
+    if (philox) {
+        switch (variant) {
+        case 13: return v3_pick<1, dev::NODES_48, 1, true>(count, tex);
+        case 22: return v4_pick<1, dev::NODES_64, 1, true>(count, tex);
+        default: return v3_pick<1, dev::NODES_48, 4, true>(count, tex);  // 25
+        }
+    }
     switch (variant) {
     case 0: return pick_count<false, dev::STACK_SCRATCH, 1>(count);
     case 1: return pick_count<false, dev::STACK_LDS, 1>(count);
@@ -1420,6 +1587,10 @@ KernelFn pick(int variant, bool count, bool tex) {
     case 20: return v4_pick<6, dev::NODES_HALF>(count, tex);
     case 21: return v3_pick<1, dev::NODES_64>(count, tex);
     case 22: return v4_pick<1, dev::NODES_64>(count, tex);
+    case 24: return v3_pick<1, dev::NODES_48, 2>(count, tex);
+    case 25: return v3_pick<1, dev::NODES_48, 4>(count, tex);
+    case 26: return v4_pick<1, dev::NODES_64, 2>(count, tex);
+    case 27: return v4_pick<1, dev::NODES_64, 4>(count, tex);
     default: return v4_pick<7, dev::NODES_64>(count, tex);
     }
 }
@@ -1525,7 +1696,8 @@ int rt_set_tuning(int key, int value) {
 int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) {
     if (!scene || !a) { set_error("rt_render: NULL scene or args"); return RT_ERR_INVALID_ARGUMENT; }
     if (a->tiling.local_rows == 0 || a->width == 0 || a->height == 0) return RT_OK;  // nothing to render
-    if (!a->state) { set_error("rt_render: state is NULL"); return RT_ERR_INVALID_ARGUMENT; }
+    const bool philox = (a->flags & RT_FLAG_RNG_PHILOX) != 0;
+    if (!a->state && !philox) { set_error("rt_render: state is NULL"); return RT_ERR_INVALID_ARGUMENT; }
     if (!a->pos && !a->radiance && !a->accum) { set_error("rt_render: no output buffer"); return RT_ERR_INVALID_ARGUMENT; }
     if ((a->flags & RT_FLAG_ACCUMULATE) && !a->accum) { set_error("rt_render: ACCUMULATE without accum"); return RT_ERR_INVALID_ARGUMENT; }
     if (a->width == 0 || a->height == 0) return RT_OK;
@@ -1578,6 +1750,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.grid_h = faithful ? (a->height / 16) * 16 : a->height;
     P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
     P.regen_threshold = (uint32_t)g_regen_threshold;
+    P.rng_key_lo = (uint32_t)a->rng_seed;
+    P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
+    P.rng_frame = a->rng_frame;
     // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
     const rt_input_struct& in = a->inputs;
     P.width_f = (float)a->width;
@@ -1617,37 +1792,47 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
     int variant = g_variant;
     // auto: the fastest measured kernel per workload shape (profiles/r01_*): the persistent v4 for short
-    // or deep paths per pixel (config 5: 1 spp, 0.54 vs 0.80 ms; config 3: depth 16, 438 vs 461 ms), v3
-    // for the many-sample frames (config 2: 64 spp, 26.1 vs 27.4 ms)
+    // or deep paths per pixel (config 5: 1 spp, 0.54 vs 0.80 ms; config 3: depth 16, 457 vs 467 ms), v3
+    // with four independent waves per workgroup for the many-sample frames (config 2: 64 spp, 25.7-26.2
+    // vs 26.5-26.9 ms for one wave per workgroup, 27.4-27.8 ms for v4)
     if (variant < 0 || variant >= kNumVariants)
-        variant = (a->samples_per_pixel < 32 || a->max_depth > 8) ? 22 : 13;
+        variant = (a->samples_per_pixel < 32 || a->max_depth > 8) ? 22 : 25;
     if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
         variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
     if (kVariants[variant].half && !S.has_half_nodes)  // a plane beyond the binary16 range: f32 boxes
         variant = variant == 18 ? 13 : (variant == 19 ? 16 : 17);
     if (kVariants[variant].persistent && (a->samples_per_pixel == 0 || a->max_depth == 0))
         variant = kVariants[variant].half ? 18 : 13;  // the persistent kernel assumes every pixel traces a ray
+    if (philox && !philox_capable(variant)) {
+        if (kVariants[variant].stack != dev::STACK_LDS16) {
+            set_error("rt_render: RT_FLAG_RNG_PHILOX needs the v3/v4 kernels (< 32767 BVH nodes, < 8192 primitives)");
+            return RT_ERR_UNSUPPORTED;
+        }
+        variant = kVariants[variant].persistent ? 22 : 13;
+    }
     const Variant& V = kVariants[variant];
     // near-first traversal holds at most one deferred child per level below the root
     if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
     }
+    // v3/v4: per wave, the parked path state + a 16-bit stack of depth + 3 entries (two sentinel pads)
+    const size_t wave_bytes = V.stack == dev::STACK_LDS16
+                                  ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::PK_WORDS) * 64 * 4 + (size_t)(S.depth + 3) * 64 * 2
+                                  : 0;
+    P.lds_wave_words = (uint32_t)(wave_bytes / 4);
     size_t lds_bytes = (V.scene_lds ? scene_lds : 0) +
-                       (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) +
-                       (V.stack == dev::STACK_LDS16
-                            ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::PK_WORDS) * 64 * 4 + (size_t)(S.depth + 3) * 64 * 2
-                            : 0);
+                       (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes * (size_t)V.wpg;
     if (lds_bytes > kLdsLimit) {
         set_error("rt_render: scene does not fit in LDS for this variant");
         return RT_ERR_UNSUPPORTED;
     }
-    KernelFn fn = pick(variant, count_tests, S.has_textures);
-    const uint32_t tile = V.block == 64 ? 8u : 16u;
+    KernelFn fn = pick(variant, count_tests, S.has_textures, philox);
+    const uint32_t tile = (V.block == 64 || V.wpg > 1) ? 8u : 16u;  // v3/v4: one 8×8 tile per wave
     P.tiles_x = (a->width + tile - 1) / tile;
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
     hipStream_t s = (hipStream_t)stream;
-    uint32_t grid = tiles;
+    uint32_t grid = (tiles + (uint32_t)V.wpg - 1) / (uint32_t)V.wpg;
     if (V.persistent) {
         int device = 0, cus = 0, per_cu = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
@@ -1659,7 +1844,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.work_total = tiles * 64u;
         if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
-        grid = (uint32_t)(resident < tiles ? resident : tiles);
+        grid = (uint32_t)(resident < grid ? resident : grid);
         rc = hip_check(hipMemsetAsync(P.work_counter, 0, sizeof(uint32_t), s), "rt_render: work queue reset");
         if (rc != RT_OK) return rc;
     }

@@ -66,7 +66,14 @@ class Renderer:
     """One rank's share of a W×H image (all of it when num_ranks = 1)."""
 
     def __init__(self, width: int, height: int, device: int | str = 0, band_rows: int | None = None,
-                 num_ranks: int = 1, rank: int = 0):
+                 num_ranks: int = 1, rank: int = 0, rng: str = "xorwow"):
+        """rng = "xorwow": the reference's per-pixel cuRAND XORWOW state (parity mode); "philox": stateless
+        per-pixel Philox4x32-10 streams (RT_FLAG_RNG_PHILOX, perf mode, no RNG bytes in HBM)."""
+        if rng not in ("xorwow", "philox"):
+            raise ValueError(f"rng must be 'xorwow' or 'philox', not {rng!r}")
+        self.rng = rng
+        self.seed = 1984  # Kernel.cu:175 seed base; the Philox key in perf mode
+        self.frame = 0    # Philox frame counter (the XORWOW streams carry over in `state` instead)
         if not torch.cuda.is_available():
             raise RTError("no HIP device visible: librt_hip.so renders on MI355X only")
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -79,8 +86,10 @@ class Renderer:
         self.local_rows = len(self.rows)
         n = width * self.local_rows
         # InitCudaBuffers (CudaLayer.cpp:68-74): RGBA8 framebuffer + one 48-byte curandState per pixel
+        # (none in Philox mode)
         self.pos = torch.zeros(n, dtype=torch.int32, device=self.device)
-        self.state = torch.zeros(n * abi.STATE_WORDS, dtype=torch.int32, device=self.device)
+        self.state = (torch.zeros(n * abi.STATE_WORDS, dtype=torch.int32, device=self.device)
+                      if rng == "xorwow" else None)
         self.counters = torch.zeros(8, dtype=torch.int64, device=self.device)
         self.radiance = None
         self.accum = None
@@ -92,14 +101,19 @@ class Renderer:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def render_init(self, seed_base: int = 1984) -> None:
-        """RenderInit: curand_init(seed_base + global pixel index, 0, 0) (Kernel.cu:166-176)."""
+        """RenderInit: curand_init(seed_base + global pixel index, 0, 0) (Kernel.cu:166-176); in Philox mode
+        the seed becomes the Philox key and the frame counter restarts."""
+        self.seed, self.frame = seed_base, 0
+        if self.state is None:
+            return
         t = self.tiling()
         check(lib().rt_render_init(C.c_void_p(self.state.data_ptr()), self.width, self.height, C.byref(t),
                                    seed_base, C.c_void_p(self.stream())), "rt_render_init")
 
     def render(self, scene: DeviceScene, spp: int, max_depth: int, inputs: abi.InputStruct, flags: int = 0,
-               radiance: bool = False, count: bool = True) -> torch.Tensor:
-        """One frame (Kernel.cu:102-158), asynchronous on torch's current stream; returns `pos`."""
+               radiance: bool = False, count: bool = True, frame: int | None = None) -> torch.Tensor:
+        """One frame (Kernel.cu:102-158), asynchronous on torch's current stream; returns `pos`.  Philox
+        mode draws frame `frame` (default: the next frame counter value) of every pixel's stream."""
         if radiance and self.radiance is None:
             self.radiance = torch.zeros(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
         if flags & abi.RT_FLAG_ACCUMULATE and self.accum is None:
@@ -108,10 +122,17 @@ class Renderer:
         a.pos = self.pos.data_ptr()
         a.radiance = self.radiance.data_ptr() if radiance else None
         a.accum = self.accum.data_ptr() if self.accum is not None and flags & abi.RT_FLAG_ACCUMULATE else None
-        a.state = self.state.data_ptr()
+        a.state = self.state.data_ptr() if self.state is not None else None
         a.counters = self.counters.data_ptr() if count else None
         a.width, a.height = self.width, self.height
         a.samples_per_pixel, a.max_depth = spp, max_depth
+        if self.rng == "philox":
+            flags |= abi.RT_FLAG_RNG_PHILOX
+            if frame is None:
+                frame = self.frame
+                if not flags & abi.RT_FLAG_NO_STATE_WRITEBACK:
+                    self.frame += 1  # the next frame draws fresh numbers, as the XORWOW streams advance
+            a.rng_seed, a.rng_frame = self.seed, frame
         a.flags = flags
         a.tiling = self.tiling()
         a.inputs = inputs

@@ -218,7 +218,13 @@ enum rt_render_flags {
     RT_FLAG_ACCUMULATE = 1u << 2, /* accum[px].rgb += Σ samples, accum[px].w += spp; pos shows rgb / w */
     RT_FLAG_RIUS_LEFT_TO_RIGHT = 1u << 3, /* fill Random()'s Vec3(ξ,ξ,ξ) left to right (default: right to
                                              left, the order the survey's g++ build of Math.cuh:233 used) */
-    RT_FLAG_COUNT_TESTS = 1u << 4 /* also count box and primitive tests into counters[1], [2] */
+    RT_FLAG_COUNT_TESTS = 1u << 4, /* also count box and primitive tests into counters[1], [2] */
+    RT_FLAG_RNG_PHILOX = 1u << 5   /* perf-mode RNG: each pixel draws from the hipRAND/rocRAND Philox4x32-10
+                                      stream rocrand_init(rng_seed, subsequence = global pixel index,
+                                      offset = rng_frame << 34) with rocrand_uniform, instead of its cuRAND
+                                      XORWOW state.  `state` is neither read nor written (may be NULL): no
+                                      per-pixel RNG bytes in HBM.  Not the reference's stream (its images
+                                      match the parity mode statistically, not bit for bit). */
 };
 
 typedef struct rt_render_args {
@@ -237,6 +243,9 @@ typedef struct rt_render_args {
     uint32_t reserved;        /* must be 0 */
     rt_tiling tiling;
     rt_input_struct inputs;
+    uint64_t rng_seed;        /* RT_FLAG_RNG_PHILOX: Philox key (e.g. 1984, the reference's seed base) */
+    uint32_t rng_frame;       /* RT_FLAG_RNG_PHILOX: frame counter; each frame draws fresh numbers */
+    uint32_t reserved2;       /* must be 0 */
 } rt_render_args;
 
 /* One frame of the per-pixel render kernel (Kernel.cu:102-158) on `stream`. */

@@ -53,7 +53,11 @@ def lib() -> C.CDLL:
         L.orc_scene_set_exact.argtypes = [vp, C.c_int]
         L.orc_render_init.argtypes = [vp, C.c_uint, C.c_uint, C.c_ulonglong, C.c_int]
         L.orc_render.argtypes = [vp, vp, vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint, vp, C.POINTER(abi.InputStruct),
-                                 C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.POINTER(Counters)]
+                                 C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_int, C.c_ulonglong,
+                                 C.c_uint, C.POINTER(Counters)]
+        L.orc_philox4x32_10.argtypes = [C.POINTER(C.c_uint), C.POINTER(C.c_uint), C.POINTER(C.c_uint)]
+        L.orc_philox_uniform_at.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_uint]
+        L.orc_philox_uniform_at.restype = C.c_float
         L.orc_hittable_hit.argtypes = [C.POINTER(abi.HittableDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.c_float, C.c_float, C.POINTER(Hit)]
         L.orc_scatter.argtypes = [C.POINTER(abi.MaterialDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -94,13 +98,17 @@ def init_states(width: int, height: int, seed_base: int = 1984, full: bool = Tru
 
 def render(oscene: OracleScene, width: int, height: int, spp: int, depth: int, inputs: abi.InputStruct,
            states: np.ndarray, faithful_grid: bool = False, rows: tuple | None = None, threads: int = 0,
-           rius_order: int = 1, radiance: bool = False, row_step: int = 1):
-    """One frame; returns (pos (H, W) uint32, radiance (H, W, 4) or None, Counters).  `states` advances."""
+           rius_order: int = 1, radiance: bool = False, row_step: int = 1, philox: bool = False,
+           seed: int = 1984, frame: int = 0):
+    """One frame; returns (pos (H, W) uint32, radiance (H, W, 4) or None, Counters).  `states` advances
+    (XORWOW mode); with philox=True the pixels draw from their (seed, pixel, frame) Philox streams and
+    `states` may be None."""
     pos = np.zeros(width * height, dtype=np.uint32)
     rad = np.zeros(width * height * 4, dtype=np.float32) if radiance else None
     cnt = Counters()
     r0, r1 = rows if rows else (0, height)
     lib().orc_render(oscene.handle, pos.ctypes.data, rad.ctypes.data if rad is not None else None, width, height,
-                     spp, depth, states.ctypes.data, C.byref(inputs), 1 if faithful_grid else 0, r0, r1, row_step, threads,
-                     rius_order, C.byref(cnt))
+                     spp, depth, states.ctypes.data if states is not None else None, C.byref(inputs),
+                     1 if faithful_grid else 0, r0, r1, row_step, threads, rius_order, 1 if philox else 0, seed, frame,
+                     C.byref(cnt))
     return pos.reshape(height, width), (rad.reshape(height, width, 4) if rad is not None else None), cnt

@@ -103,11 +103,65 @@ float orc_curand_uniform(rt_curand_state* s) {
     return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
 }
 
+/* ---------------------------------------------------------------------------------------------- */
+/* Philox4x32-10: the perf-mode RNG BASELINE.json's north_star names ("hiprand (Philox) per-pixel   */
+/* state").  Restates rocRAND's philox4x32_10_engine (/opt/rocm/include/rocrand/                    */
+/* rocrand_philox4x32_10.h:270-303, the Random123 round) and rocrand_uniform (rocrand_uniform.h:    */
+/* 65-68, 239-242).  A pixel's stream is rocrand_init(seed, subsequence = global pixel index,        */
+/* offset = frame << 34): draw n of a frame is word n & 3 of philox10(ctr = {n >> 2, frame, pixel,  */
+/* 0}, key = {seed lo, seed hi}).  Pinned by tests/golden/philox_kat.json (rocRAND's own engine).   */
+/* ---------------------------------------------------------------------------------------------- */
+void orc_philox4x32_10(const unsigned int ctr_in[4], const unsigned int key_in[2], unsigned int out[4]) {
+    unsigned int c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    unsigned int k0 = key_in[0], k1 = key_in[1];
+    for (int round = 0; round < 10; round++) {
+        unsigned long long m0 = 0xD2511F53ull * (unsigned long long)c0;
+        unsigned long long m1 = 0xCD9E8D57ull * (unsigned long long)c2;
+        unsigned int hi0 = (unsigned int)(m0 >> 32), lo0 = (unsigned int)m0;
+        unsigned int hi1 = (unsigned int)(m1 >> 32), lo1 = (unsigned int)m1;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+        k0 += 0x9E3779B9u; /* bumpkey */
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* uniform in (0, 1]: 2^-32 + x·2^-32 (rocrand_uniform.h:65-68).  x·2^-32 is exact, so a fused and an
+ * unfused evaluation agree. */
+static inline float philox_to_uniform(unsigned int x) { return 2.3283064e-10f + (float)x * 2.3283064e-10f; }
+
+float orc_philox_uniform_at(unsigned long long seed, unsigned int pixel, unsigned int frame, unsigned int n) {
+    unsigned int ctr[4] = {n >> 2, frame, pixel, 0u};
+    unsigned int key[2] = {(unsigned int)seed, (unsigned int)(seed >> 32)};
+    unsigned int r[4];
+    orc_philox4x32_10(ctr, key, r);
+    return philox_to_uniform(r[n & 3u]);
+}
+
+/* The RNG of one pixel: the reference's cuRAND XORWOW state (parity mode) or a Philox stream. */
+typedef struct {
+    int philox;
+    rt_curand_state* xs;
+    unsigned int key[2], frame, pixel, n, r[4];
+} orc_rng;
+
+static float orc_uniform(orc_rng* g) {
+    if (!g->philox) return orc_curand_uniform(g->xs);
+    if ((g->n & 3u) == 0u) {
+        unsigned int ctr[4] = {g->n >> 2, g->frame, g->pixel, 0u};
+        orc_philox4x32_10(ctr, g->key, g->r);
+    }
+    return philox_to_uniform(g->r[g->n++ & 3u]);
+}
+
 /* Random() (Math.cuh:231-234) + RandomInUnitSphere (Math.cuh:252-260). */
-static inline v3 random_in_unit_sphere(rt_curand_state* st, int order, int* draws) {
+static inline v3 random_in_unit_sphere(orc_rng* st, int order, int* draws) {
     v3 p;
     do {
-        float a = orc_curand_uniform(st), b = orc_curand_uniform(st), c = orc_curand_uniform(st);
+        float a = orc_uniform(st), b = orc_uniform(st), c = orc_uniform(st);
         v3 r = order == 0 ? mk(a, b, c) : mk(c, b, a);
         *draws += 3;
         p = sub(scale(2.0f, r), mk(1.0f, 1.0f, 1.0f));
@@ -445,7 +499,7 @@ static v3 texture_value(const orc_scene* s, const rt_texture_desc* t, float u, f
 
 /* Scatter of Lambertian (:43-62), Metal (:75-94), Dielectric (:106-145).  Returns the flag. */
 static int scatter(const orc_scene* s, const rt_material_desc* m, v3 ro, v3 rd, const hitrec* rec,
-                   rt_curand_state* st, v3* so, v3* sd, v3* att, int* draws, int order) {
+                   orc_rng* st, v3* so, v3* sd, v3* att, int* draws, int order) {
     (void)ro;
     switch (m->type) {
     case RT_LAMBERTIAN: {
@@ -494,7 +548,7 @@ static int scatter(const orc_scene* s, const rt_material_desc* m, v3 ro, v3 rd, 
         }
         *draws += 1;
         *so = rec->p;
-        *sd = orc_curand_uniform(st) < reflect_prob ? reflected : refracted;
+        *sd = orc_uniform(st) < reflect_prob ? reflected : refracted;
         return 1;
     }
     default: return 0; /* DiffuseLight::Scatter (:158-162) */
@@ -502,7 +556,7 @@ static int scatter(const orc_scene* s, const rt_material_desc* m, v3 ro, v3 rd, 
 }
 
 /* color() (Kernel.cu:30-80) */
-static v3 color(const orc_scene* s, v3 o, v3 d, int max_depth, rt_curand_state* st, const rt_input_struct* in,
+static v3 color(const orc_scene* s, v3 o, v3 d, int max_depth, orc_rng* st, const rt_input_struct* in,
                 int order, orc_counters* c) {
     v3 cur_att = mk(1.0f, 1.0f, 1.0f);
     v3 black = mk(0.0f, 0.0f, 0.0f);
@@ -565,7 +619,7 @@ void orc_render_init(rt_curand_state* state, unsigned width, unsigned height, un
 void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, unsigned width, unsigned height,
                 unsigned spp, unsigned max_depth, rt_curand_state* state, const rt_input_struct* in,
                 int faithful_grid, unsigned row_begin, unsigned row_end, unsigned row_step, int threads,
-                int order, orc_counters* counters) {
+                int order, int philox, unsigned long long seed, unsigned frame, orc_counters* counters) {
     unsigned gw = faithful_grid ? (width / 16) * 16 : width;
     unsigned gh = faithful_grid ? (height / 16) * 16 : height;
     if (row_end > gh) row_end = gh;
@@ -584,19 +638,31 @@ void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, unsigned
         orc_counters c = {0, 0, 0, 0};
         for (int x = 0; x < (int)gw; x++) {
             unsigned pixel_index = (unsigned)y * width + (unsigned)x;
-            rt_curand_state st = state[pixel_index];
+            rt_curand_state st;
+            orc_rng g;
+            memset(&g, 0, sizeof(g));
+            if (philox) { /* no per-pixel state in HBM: the stream is a function of (seed, pixel, frame) */
+                g.philox = 1;
+                g.key[0] = (unsigned)seed;
+                g.key[1] = (unsigned)(seed >> 32);
+                g.frame = frame;
+                g.pixel = pixel_index;
+            } else {
+                st = state[pixel_index];
+                g.xs = &st;
+            }
             v3 col = mk(0.0f, 0.0f, 0.0f);
             for (unsigned smp = 0; smp < spp; smp++) {
-                float u = ((float)((float)x - center.x) + orc_curand_uniform(&st)) / (float)width;
-                float v = ((float)(center.y - (float)y) + orc_curand_uniform(&st)) / (float)width;
+                float u = ((float)((float)x - center.x) + orc_uniform(&g)) / (float)width;
+                float v = ((float)(center.y - (float)y) + orc_uniform(&g)) / (float)width;
                 v3 dist = add(scale(u, right), scale(v, up));
                 v3 start = add(add(scale(in->near_plane, dist), origin), scale(in->fov, fwd));
                 v3 second = add(add(scale(in->far_plane, dist), scale(1.0f / in->fov * 10.0f, fwd)), origin);
                 v3 dir = normalize(sub(second, start));
                 c.primary++;
-                col = add(col, color(s, start, dir, (int)max_depth, &st, in, order, &c));
+                col = add(col, color(s, start, dir, (int)max_depth, &g, in, order, &c));
             }
-            state[pixel_index] = st;
+            if (!philox) state[pixel_index] = st;
             col = divs(col, (float)spp);
             if (radiance) {
                 float* rp = radiance + 4 * (size_t)pixel_index;
@@ -644,7 +710,10 @@ int orc_scatter(const rt_material_desc* m, const float o[3], const float d[3], c
     v3 o3, d3, a3 = mk(0.0f, 0.0f, 0.0f);
     o3 = d3 = a3;
     *draws = 0;
-    int r = scatter(&s, m, ld3(o), ld3(d), &rec, st, &o3, &d3, &a3, draws, order);
+    orc_rng g;
+    memset(&g, 0, sizeof(g));
+    g.xs = st;
+    int r = scatter(&s, m, ld3(o), ld3(d), &rec, &g, &o3, &d3, &a3, draws, order);
     so[0] = o3.x; so[1] = o3.y; so[2] = o3.z;
     sd[0] = d3.x; sd[1] = d3.y; sd[2] = d3.z;
     att[0] = a3.x; att[1] = a3.y; att[2] = a3.z;

@@ -26,6 +26,11 @@ void orc_curand_init(unsigned long long seed, rt_curand_state* state);
 unsigned int orc_curand(rt_curand_state* state);
 float orc_curand_uniform(rt_curand_state* state);
 
+/* Philox4x32-10 (rocRAND philox4x32_10_engine / rocrand_uniform): ten rounds of the Random123 function,
+ * and draw n of the (seed, pixel, frame) stream the perf-mode kernel uses (RT_FLAG_RNG_PHILOX). */
+void orc_philox4x32_10(const unsigned int ctr[4], const unsigned int key[2], unsigned int out[4]);
+float orc_philox_uniform_at(unsigned long long seed, unsigned int pixel, unsigned int frame, unsigned int n);
+
 /* Reference BVH (Hittable.cuh:303-385) over the scene's active hittables. */
 orc_scene* orc_scene_build(const rt_scene_desc* desc);
 void orc_scene_free(orc_scene* s);
@@ -51,11 +56,13 @@ typedef struct orc_counters {
  * (bounded CPU-baseline samples; row_step 0 = 1).
  * faithful_grid: skip pixels outside whole 16×16 blocks (Kernel.cu:184).  threads: OpenMP threads (0 =
  * default).  rius_order: 0 = left-to-right evaluation of Vec3(ξ,ξ,ξ) in Random() (Math.cuh:231-234),
- * 1 = right-to-left (what g++ emits for that constructor call). */
+ * 1 = right-to-left (what g++ emits for that constructor call).  philox != 0: every pixel draws from the
+ * Philox stream (seed, global pixel index, frame) instead of its XORWOW state; `state` is not used and may
+ * be NULL. */
 void orc_render(const orc_scene* scene, unsigned int* pos, float* radiance, unsigned width, unsigned height,
                 unsigned spp, unsigned max_depth, rt_curand_state* state, const rt_input_struct* inputs,
                 int faithful_grid, unsigned row_begin, unsigned row_end, unsigned row_step, int threads,
-                int rius_order, orc_counters* counters);
+                int rius_order, int philox, unsigned long long seed, unsigned frame, orc_counters* counters);
 
 /* Known-answer helpers. */
 typedef struct orc_hit {

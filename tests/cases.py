@@ -48,3 +48,6 @@ CASES = [
     Case("c2_rtiow_ragged_100x37_s4", "c2", 100, 37, 4),
 ]
 CASE_BY_NAME = {c.name: c for c in CASES}
+
+# Perf-mode RNG (RT_FLAG_RNG_PHILOX) fixtures: (case, frame index), seed 1984.
+PHILOX_CASES = [(CASE_BY_NAME["c2_rtiow_ltr_96x64_s8"], 3), (CASE_BY_NAME["c3_cornell_128_s16"], 0)]

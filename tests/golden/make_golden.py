@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(HERE))
 
-from cases import CASES  # noqa: E402
+from cases import CASES, PHILOX_CASES  # noqa: E402
 from cudaraytracer_amd import abi, scenes  # noqa: E402
 from oracle import py_oracle as po  # noqa: E402
 
@@ -73,6 +73,18 @@ def main() -> None:
             texture_sha256=np.frombuffer(digest(np.asarray(sc.images[0]) if sc.images else np.zeros(0, np.uint8)),
                                          np.uint8))
         print(case.name, pos.shape, cnt.rays, flush=True)
+    for case, frame in PHILOX_CASES:
+        cfg = case.cfg()
+        sc = scenes.builtin(cfg.scene)
+        pos, rad, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), None,
+                                  faithful_grid=case.faithful_grid, rius_order=case.rius_order, radiance=True,
+                                  philox=True, seed=1984, frame=frame)
+        np.savez_compressed(
+            os.path.join(HERE, f"philox_{case.name}_f{frame}.npz"),
+            inputs=np.frombuffer(bytes(cfg.inputs()), np.uint8), pos=pos,
+            radiance_sha256=np.frombuffer(digest(rad), np.uint8),
+            counters=np.array([cnt.rays, cnt.box_tests, cnt.prim_tests, cnt.primary], np.uint64))
+        print("philox", case.name, frame, cnt.rays, flush=True)
 
 
 if __name__ == "__main__":

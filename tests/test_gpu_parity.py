@@ -14,7 +14,7 @@ import pytest
 import torch
 
 import refgraph
-from cases import CASE_BY_NAME, CASES
+from cases import CASE_BY_NAME, CASES, PHILOX_CASES
 from cudaraytracer_amd import abi, scenes
 from cudaraytracer_amd._lib import RTError, lib
 from cudaraytracer_amd.renderer import DeviceScene, Renderer
@@ -23,7 +23,7 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = list(range(24))
+VARIANTS = list(range(28))
 # v3 (13), persistent v4 (16), binary16 nodes (18), persistent + binary16 (19)
 KEY_VARIANTS = [13, 16, 18, 19]
 
@@ -355,3 +355,96 @@ def test_scene_beyond_binary16_range_matches_oracle(variant):
     ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
     np.testing.assert_array_equal(r.image(), ref)
     assert int(r.counters[0]) == cnt.rays
+
+
+# ---------------------------------------------------------------------------------------------------
+# Perf-mode RNG (RT_FLAG_RNG_PHILOX): bit-exact with the oracle's Philox restatement, no state buffer
+# ---------------------------------------------------------------------------------------------------
+PHILOX_KERNELS = [-1, 13, 22, 25, 16]  # auto, v3, v4, v3 × 4 waves/WG; 16 (no Philox build) maps to 22
+
+
+@pytest.mark.parametrize("variant", PHILOX_KERNELS)
+@pytest.mark.parametrize("case", [CASE_BY_NAME[n] for n in ("c1_full", "c2_rtiow_192x112_s16", "c3_cornell_128_s16",
+                                                            "c5_textured_160x96_s4", "c2_rtiow_ragged_100x37_s4",
+                                                            "c2_rtiow_ltr_96x64_s8")], ids=lambda c: c.name)
+def test_philox_bit_exact_vs_oracle(case, variant):
+    cfg = case.cfg()
+    lib().rt_set_variant(variant)
+    sc = scenes.builtin(cfg.scene)
+    r = Renderer(cfg.width, cfg.height, rng="philox")
+    assert r.state is None
+    r.render_init()
+    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags, radiance=True, frame=5)
+    torch.cuda.synchronize()
+    ref, rad, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), None,
+                              faithful_grid=case.faithful_grid, rius_order=case.rius_order, radiance=True,
+                              philox=True, seed=1984, frame=5)
+    if case.faithful_grid:  # pixels outside whole 16×16 blocks are not written (Kernel.cu:184)
+        gh, gw = (cfg.height // 16) * 16, (cfg.width // 16) * 16
+        np.testing.assert_array_equal(r.image()[:gh, :gw], ref[:gh, :gw])
+    else:
+        np.testing.assert_array_equal(r.image(), ref)
+        np.testing.assert_array_equal(r.radiance_image(), rad)
+    assert int(r.counters[0]) == cnt.rays
+
+
+@pytest.mark.parametrize("case, frame", PHILOX_CASES, ids=lambda x: getattr(x, "name", str(x)))
+def test_philox_matches_golden(case, frame):
+    g = load_golden(f"philox_{case.name}_f{frame}")
+    cfg = case.cfg()
+    r = Renderer(cfg.width, cfg.height, rng="philox")
+    r.render_init(1984)
+    r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags, frame=frame)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r.image(), g["pos"])
+    assert int(r.counters[0]) == int(g["counters"][0])
+
+
+def test_philox_frames_tiles_and_invalid_state():
+    case = CASE_BY_NAME["c2_rtiow_192x112_s16"]
+    cfg = case.cfg()
+    ds = DeviceScene(scenes.builtin(cfg.scene))
+    r = Renderer(cfg.width, cfg.height, rng="philox")
+    r.render_init()
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())  # frame 0
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())  # frame 1: fresh numbers
+    torch.cuda.synchronize()
+    f1 = r.image().copy()
+    assert r.frame == 2
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), frame=0)
+    torch.cuda.synchronize()
+    f0 = r.image().copy()
+    assert image_stats(f0, f1)["exact"] < 0.9
+    # block-cyclic bands reassemble into the 1-rank frame (global pixel index keys the streams)
+    full = np.zeros_like(f0)
+    for rank in range(3):
+        rr = Renderer(cfg.width, cfg.height, band_rows=16, num_ranks=3, rank=rank, rng="philox")
+        rr.render_init()
+        rr.render(ds, cfg.spp, cfg.depth, cfg.inputs(), frame=0)
+        torch.cuda.synchronize()
+        full[rr.rows] = rr.image()
+    np.testing.assert_array_equal(full, f0)
+    # XORWOW mode still refuses a NULL state
+    a = abi.RenderArgs()
+    a.pos, a.width, a.height, a.samples_per_pixel, a.max_depth = r.pos.data_ptr(), cfg.width, cfg.height, 1, 1
+    a.tiling = abi.Tiling(cfg.height, 1, 0, cfg.height)
+    assert lib().rt_render(ds.handle, C.byref(a), None) == -1
+    a.flags = abi.RT_FLAG_RNG_PHILOX
+    assert lib().rt_render(ds.handle, C.byref(a), None) == 0
+    torch.cuda.synchronize()
+
+
+def test_philox_full_size_c2_rows_match_oracle():
+    cfg = scenes.CONFIGS["c2"]
+    sc = scenes.builtin(cfg.scene)
+    r = Renderer(cfg.width, cfg.height, rng="philox")
+    r.render_init()
+    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), frame=11)
+    torch.cuda.synchronize()
+    step = cfg.height // 5
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), None,
+                          rows=(2, cfg.height), row_step=step, threads=16, philox=True, frame=11)
+    rows = list(range(2, cfg.height, step))
+    np.testing.assert_array_equal(r.image()[rows], ref[rows])
+    rays = int(r.counters[0])
+    assert 2.9 < rays / (cfg.width * cfg.height * cfg.spp) < 3.3
