@@ -198,6 +198,7 @@ template <> struct StackOf<STACK_HYBRID> { using T = HybridStack; };
 struct Counts {
     uint32_t rays, boxes, prims, primary;
     uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
+    uint64_t ctrav = 0, cshade = 0, ctotal = 0, cleaf = 0;  // COUNT_TESTS (v3): wave clock cycles per phase
 };
 
 // 1 on the lowest active lane of the wave, 0 elsewhere (diagnostic wave-iteration counts).
@@ -544,6 +545,12 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt
             atomicAdd(&P.counters[4], (unsigned long long)cnt.wnode);
             atomicAdd(&P.counters[5], (unsigned long long)cnt.wleaf);
             atomicAdd(&P.counters[6], (unsigned long long)cnt.wshade);
+            if (cnt.ctotal && wave_leader()) {  // one lane per wave: the stamps are wave-uniform
+                atomicAdd(&P.counters[7], (unsigned long long)cnt.ctrav);
+                atomicAdd(&P.counters[8], (unsigned long long)cnt.cshade);
+                atomicAdd(&P.counters[9], (unsigned long long)cnt.ctotal);
+                atomicAdd(&P.counters[10], (unsigned long long)cnt.cleaf);
+            }
         }
         atomicAdd(&P.counters[3], (unsigned long long)cnt.primary);
     }
@@ -1154,6 +1161,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             sp = nsp;
             if (__ballot(leaf == 0) == 0) break;
         }
+        const uint64_t t_leaf = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         while (leaf < 0) {
             const uint32_t l = ~(uint32_t)leaf;
             const uint32_t first = l >> 2, count = (l & 3u) + 1u;
@@ -1207,6 +1215,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 sp = sp > kStackBase ? sp - 1u : kStackBase;
             }
         }
+        if (COUNT_TESTS) cnt.cleaf += __builtin_amdgcn_s_memtime() - t_leaf;
         if ((uint32_t)__popcll(__ballot(1)) < threshold) break;
     }
     c.node = node;
@@ -1261,10 +1270,14 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
     }
     const uint32_t threshold = P.regen_threshold;
 
+    const uint64_t t_start = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
     while (true) {
+        const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (c.mode == MODE_TRAV) {
             v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, prims, stk, threshold, ro, rd, c, cnt);
         }
+        const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
         if (c.mode == MODE_SHADE) {
             R rng;
             f3 col, att;
@@ -1284,8 +1297,10 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
             }
             v3_park(park, rng, col, att, sample, depth, rays);
         }
+        if (COUNT_TESTS) cnt.cshade += __builtin_amdgcn_s_memtime() - t_b;
         if (__ballot(c.mode != MODE_DONE) == 0) break;
     }
+    if (COUNT_TESTS) cnt.ctotal = __builtin_amdgcn_s_memtime() - t_start;
     R rng;
     f3 col, att;
     uint32_t sample, depth, rays;

@@ -90,7 +90,7 @@ class Renderer:
         self.pos = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.state = (torch.zeros(n * abi.STATE_WORDS, dtype=torch.int32, device=self.device)
                       if rng == "xorwow" else None)
-        self.counters = torch.zeros(8, dtype=torch.int64, device=self.device)
+        self.counters = torch.zeros(16, dtype=torch.int64, device=self.device)
         self.radiance = None
         self.accum = None
 

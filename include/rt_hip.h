@@ -232,9 +232,10 @@ typedef struct rt_render_args {
     float* radiance;          /* optional device float[local_rows·width·4]: pre-gamma mean colour (col/spp) */
     float* accum;             /* RT_FLAG_ACCUMULATE: device float4 running sum of samples */
     rt_curand_state* state;   /* device RNG states, local_rows × width */
-    uint64_t* counters;       /* optional device uint64[8]: rays, box tests, primitive tests, primary samples;
+    uint64_t* counters;       /* optional device uint64[16]: rays, box tests, primitive tests, primary samples;
                                  with RT_FLAG_COUNT_TESTS also [4..6] = wave-level iterations of node visits,
-                                 primitive tests and shading (SIMD-efficiency diagnostics) */
+                                 primitive tests and shading (SIMD-efficiency diagnostics) and, for the v3
+                                 kernels, [7..9] = wave clock cycles spent tracing, shading, in total */
     uint32_t width;
     uint32_t height;          /* global image height */
     uint32_t samples_per_pixel;

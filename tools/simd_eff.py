@@ -18,4 +18,6 @@ for v in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "6,8").split(",
     rays, boxes, prims, prim_s, wn, wl, ws = c[0], c[1], c[2], c[3], c[4], c[5], c[6]
     print(f"variant {v}: rays {rays} node-visits/ray {boxes/2/rays:.2f} prim-tests/ray {prims/rays:.2f} | "
           f"SIMD eff: node {boxes/2/(64*wn):.3f} leaf {prims/(64*wl):.3f} shade {rays/(64*ws):.3f} | "
-          f"wave-iters per 64 rays: node {64*wn/rays:.1f} leaf {64*wl/rays:.1f} shade {64*ws/rays:.2f}", flush=True)
+          f"wave-iters per 64 rays: node {64*wn/rays:.1f} leaf {64*wl/rays:.1f} shade {64*ws/rays:.2f} | "
+          f"wave time: trace {c[7]/max(1,c[9]):.3f} (leaf {c[10]/max(1,c[9]):.3f}) shade {c[8]/max(1,c[9]):.3f} "
+          f"cycles per 64 rays {64*c[9]/rays:.0f}", flush=True)
