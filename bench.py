@@ -82,13 +82,19 @@ def philox_mode(cfg: scenes.Config, scene: DeviceScene, inputs, steps: int) -> d
             "rays_per_frame": int(rays), "hbm_rng_state_bytes": 0}
 
 
-def pmc_traffic(config: str, n_gpus: int):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{config}_n{n_gpus}.json")
+def pmc_profile(config: str, rng: str) -> dict:
+    """HBM bytes per launch and SIMD-efficiency counters of the default kernel from the committed rocprofv3
+    PMC summary (profiles/pmc_<config>_n1.json, tools/profile_pmc.sh), or {}.  Under weak scaling every
+    rank launches the same 1920x1080-sized share, so the N=1 per-launch figures apply per rank."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}_n1.json")
     if not os.path.exists(path):
-        return None
+        return {}
     with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        d = json.load(f)
+    d = d.get("philox", {}) if rng == "philox" else d
+    keys = ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch", "valu_lane_utilization", "avg_waves_per_simd",
+            "ta_busy_frac_per_cu", "kernel")
+    return {k: d[k] for k in keys if k in d}
 
 
 def main() -> None:
@@ -171,6 +177,7 @@ def main() -> None:
 
     if rank == 0:
         achieved = f_launch / (kernel_ms * 1e-3) / 1e12
+        pmc = pmc_profile(args.config, args.rng) if args.config == "c2" else {}
         rays_per_launch = c[0]
         line = {
             "metric": "Mray/s (and ms/frame) at 1920x1080, 64 spp, depth 8, random-spheres",
@@ -201,7 +208,14 @@ def main() -> None:
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                "traffic": pmc_traffic(args.config, world),
+                "traffic": pmc.get("hbm_bytes_per_launch"),
+                "traffic_source": "rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_c2_n1.json" if pmc else None,
+                "algorithmic_hbm_bytes": pmc.get("algorithmic_bytes_per_launch"),
+                "hbm_GBps_achieved": (round(pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 2)
+                                      if "hbm_bytes_per_launch" in pmc else None),
+                "simd_lane_utilization": pmc.get("valu_lane_utilization"),
+                "waves_per_simd": pmc.get("avg_waves_per_simd"),
+                "ta_busy_frac": pmc.get("ta_busy_frac_per_cu"),
                 "flop_per_launch": f_launch,
                 "flop_per_ray_exec": round(f_launch / max(1, c[0]), 1),
                 "flop_per_ray_ref_bvh": round(F_REF_PER_RAY, 1),

@@ -10,11 +10,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--variant", type=int, default=-1)
 ap.add_argument("--frames", type=int, default=2)
+ap.add_argument("--rng", default="xorwow", choices=("xorwow", "philox"))
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 lib().rt_set_variant(args.variant)
 ds = DeviceScene(scenes.builtin(cfg.scene))
-r = Renderer(cfg.width, cfg.height)
+r = Renderer(cfg.width, cfg.height, rng=args.rng)
 r.render_init()
 for _ in range(args.frames):
     r.render(ds, cfg.spp, cfg.depth, cfg.inputs())

@@ -18,7 +18,7 @@ i=0
 while read -r group; do
   [ -z "$group" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex render_kernel -d "$OUT/g$i" -o p --output-format csv -- python3 tools/one_frame.py --variant "$V" --frames 1 > "$OUT/g$i.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex render_kernel -d "$OUT/g$i" -o p --output-format csv -- python3 tools/one_frame.py --variant "$V" --frames 1 ${ONE_FRAME_ARGS:-} > "$OUT/g$i.log" 2>&1
   rc=$?; echo "group $i ($group) rc=$rc" >> "$OUT/summary.txt"
   if [ $rc -ge 124 ]; then exit $rc; fi
 done <<< "$GROUPS_TEXT"
