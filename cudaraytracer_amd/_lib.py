@@ -29,6 +29,8 @@ EXPORTED = [
     "rt_render_init",
     "rt_render",
     "rt_set_timing",
+    "rt_set_wave_trace",
+    "rt_set_tile_order",
     "rt_last_kernel_ms",
     "rt_set_variant",
     "rt_set_tuning",
@@ -62,6 +64,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_render_init.argtypes = [vp, C.c_uint32, C.c_uint32, P(abi.Tiling), C.c_uint64, vp]
     lib.rt_render.argtypes = [vp, P(abi.RenderArgs), vp]
     lib.rt_set_timing.argtypes = [C.c_int]
+    lib.rt_set_wave_trace.argtypes = [C.c_void_p]
+    lib.rt_set_tile_order.argtypes = [C.c_void_p]
     lib.rt_last_kernel_ms.restype = C.c_float
     lib.rt_set_variant.argtypes = [C.c_int]
     lib.rt_set_tuning.argtypes = [C.c_int, C.c_int]

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <type_traits>
 
@@ -144,6 +145,10 @@ struct KParams {
     uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
     uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
     uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
+    unsigned long long* wave_trace;  // diagnostic (v3): per tile {start, end} of s_memrealtime (100 MHz)
+    const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
+    uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
+    uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
 };
 
 constexpr int kStackMax = 64;
@@ -982,6 +987,11 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void render_kernel_v2(const 
 constexpr int kSentinel16 = 0x7fff;
 constexpr uint32_t kStackBase = 2;  // v3 stack entries start above two sentinel pads
 enum ParkSlot { PK_RNG = 0, PK_COL = 6, PK_ATT = 9, PK_SAMPLE = 12, PK_DEPTH = 13, PK_RAYS = 14, PK_WORDS = 15 };
+// Compact parking (v3, COMPACT): sample (13 bits), depth (6 bits) and the lane's ray count (13 bits) share
+// word PK_SD, so a wave parks 13 words instead of 15 — less LDS per wave, more resident waves (the v3
+// kernels are LDS-limited).  Valid when spp < 8192, max_depth < 64 and spp · max_depth < 8192.
+enum ParkSlotCompact { PK_SD = 12, PK_WORDS_COMPACT = 13 };
+__host__ __device__ constexpr int park_words(bool compact) { return compact ? PK_WORDS_COMPACT : PK_WORDS; }
 
 // Traversal cursor of one lane (v3).
 struct Cursor {
@@ -1048,10 +1058,11 @@ __device__ __forceinline__ void unpark_rng(const uint32_t* park, RngPhilox& r) {
                   park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
 }
 
-template <class R>
+template <bool COMPACT = false, class R>
 __device__ __forceinline__ void v3_park(uint32_t* park, const R& rng, f3 col, f3 att, uint32_t sample,
                                         uint32_t depth, uint32_t rays) {
-    park[PK_RAYS * 64] = rays;
+    if constexpr (COMPACT) park[PK_SD * 64] = sample | (depth << 13) | (rays << 19);
+    else park[PK_RAYS * 64] = rays;
     park_rng(park, rng);
     park[(PK_COL + 0) * 64] = __float_as_uint(col.x);
     park[(PK_COL + 1) * 64] = __float_as_uint(col.y);
@@ -1059,21 +1070,32 @@ __device__ __forceinline__ void v3_park(uint32_t* park, const R& rng, f3 col, f3
     park[(PK_ATT + 0) * 64] = __float_as_uint(att.x);
     park[(PK_ATT + 1) * 64] = __float_as_uint(att.y);
     park[(PK_ATT + 2) * 64] = __float_as_uint(att.z);
-    park[PK_SAMPLE * 64] = sample;
-    park[PK_DEPTH * 64] = depth;
+    if constexpr (!COMPACT) {
+        park[PK_SAMPLE * 64] = sample;
+        park[PK_DEPTH * 64] = depth;
+    }
 }
 
-template <class R>
+template <bool COMPACT = false, class R>
 __device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col, f3& att, uint32_t& sample,
                                           uint32_t& depth, uint32_t& rays) {
-    rays = park[PK_RAYS * 64];
+    if constexpr (COMPACT) {
+        const uint32_t sd = park[PK_SD * 64];
+        sample = sd & 0x1fffu;
+        depth = (sd >> 13) & 0x3fu;
+        rays = sd >> 19;
+    } else {
+        rays = park[PK_RAYS * 64];
+    }
     unpark_rng(park, rng);
     col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
              __uint_as_float(park[(PK_COL + 2) * 64]));
     att = mk(__uint_as_float(park[(PK_ATT + 0) * 64]), __uint_as_float(park[(PK_ATT + 1) * 64]),
              __uint_as_float(park[(PK_ATT + 2) * 64]));
-    sample = park[PK_SAMPLE * 64];
-    depth = park[PK_DEPTH * 64];
+    if constexpr (!COMPACT) {
+        sample = park[PK_SAMPLE * 64];
+        depth = park[PK_DEPTH * 64];
+    }
 }
 
 // Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
@@ -1232,14 +1254,15 @@ __device__ __forceinline__ uint32_t* wave_lds(float4* lds, const KParams& P) {
     return (uint32_t*)lds + (threadIdx.x >> 6) * P.lds_wave_words;
 }
 
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48, int WPG = 1, bool PHILOX = false>
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48, int WPG = 1, bool PHILOX = false,
+          bool COMPACT = false>
 __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t* const wl = wave_lds(lds, P);
     uint32_t* const park = wl + lane;                                                  // word k: park[k * 64]
-    int16_t* const stk = reinterpret_cast<int16_t*>(wl + PK_WORDS * 64) + lane;        // stk[j * 64]
+    int16_t* const stk = reinterpret_cast<int16_t*>(wl + park_words(COMPACT) * 64) + lane;  // stk[j * 64]
     // node boxes and packed child references through buffer descriptors: 32-bit offsets, no 64-bit
     // address arithmetic per visit; 48 B of boxes + 4 B of references per node
     const __amdgpu_buffer_rsrc_t nrsrc =
@@ -1251,7 +1274,9 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
     const float4* __restrict__ prims = P.prims;
     uint32_t x, g;
     size_t pix;
-    if (!lane_pixel<64>(P, x, g, pix, blockIdx.x * WPG + (threadIdx.x >> 6))) return;
+    const uint32_t slot = blockIdx.x * WPG + (threadIdx.x >> 6);
+    const uint32_t tile = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
+    if (!lane_pixel<64>(P, x, g, pix, tile)) return;
     const bool rtl = P.rius_rtl != 0;
     stk[0] = (int16_t)kSentinel16;  // two sentinel pads below the stack: popping an empty stack yields
     stk[64] = (int16_t)kSentinel16;  // kSentinel16 without a bounds test
@@ -1266,11 +1291,13 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
         f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
         uint32_t sample = (uint32_t)-1, depth = 0, rays = 0;
         if (P.spp > 0) v3_next_sample(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
-        v3_park(park, rng, col, att, sample, depth, rays);  // (col + 0 = +0 above)
+        v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);  // (col + 0 = +0 above)
     }
     const uint32_t threshold = P.regen_threshold;
 
     const uint64_t t_start = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+    const uint64_t w_start = __builtin_amdgcn_s_memtime();
     while (true) {
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (c.mode == MODE_TRAV) {
@@ -1282,7 +1309,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
             R rng;
             f3 col, att;
             uint32_t sample, depth, rays;
-            v3_unpark(park, rng, col, att, sample, depth, rays);
+            v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
             bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.t_best, ro, rd, att, rng, rtl, contrib);
@@ -1295,16 +1322,24 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
             } else {
                 v3_start_trace(P.num_nodes, c, rays);
             }
-            v3_park(park, rng, col, att, sample, depth, rays);
+            v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);
         }
         if (COUNT_TESTS) cnt.cshade += __builtin_amdgcn_s_memtime() - t_b;
         if (__ballot(c.mode != MODE_DONE) == 0) break;
     }
     if (COUNT_TESTS) cnt.ctotal = __builtin_amdgcn_s_memtime() - t_start;
+    if (P.wave_trace && wave_leader()) {
+        P.wave_trace[2 * tile] = rt_start;
+        P.wave_trace[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (P.tile_cost && wave_leader()) {  // this tile's cost for the next launch's longest-first order
+        const uint64_t c = (__builtin_amdgcn_s_memtime() - w_start) >> 8;
+        P.tile_cost[tile] = c > 0xffffffffull ? 0xffffffffu : (uint32_t)c;
+    }
     R rng;
     f3 col, att;
     uint32_t sample, depth, rays;
-    v3_unpark(park, rng, col, att, sample, depth, rays);
+    v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
     cnt.rays = rays;
     cnt.primary = P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
     finish_pixel<COUNT_TESTS>(P, pix, P.state + pix * 12, rng, col, cnt);
@@ -1489,6 +1524,38 @@ __global__ void render_init_grid_kernel(uint32_t* state, uint32_t width, uint32_
     curand_init_state(1984ull + pixel_index, state + (size_t)pixel_index * 12);
 }
 
+// Longest-first launch order.  Wave lifetimes differ several-fold between tiles (glass and metal paths
+// run to depth 8, sky pixels end at once), and a frame's last waves otherwise run on a nearly empty GPU:
+// in a row-major launch the final quarter of a config-2 frame holds < 50 % of the steady-state waves.
+// After each launch this one-workgroup kernel buckets the tiles by the lifetime their wave just measured
+// (4 buckets per octave, most expensive first) into the order the next launch with the same tile grid
+// dispatches them in.  The order changes when waves start, never what they compute.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t c) {  // 0 = most expensive
+    if (c == 0u) return 127u;
+    const uint32_t msb = 31u - (uint32_t)__clz(c);
+    const uint32_t frac = msb >= 2u ? (c >> (msb - 2u)) & 3u : (c << (2u - msb)) & 3u;
+    return 127u - (msb * 4u + frac);
+}
+
+__global__ __launch_bounds__(1024) void plan_order_kernel(const uint32_t* __restrict__ cost,
+                                                          uint32_t* __restrict__ order, uint32_t n) {
+    __shared__ uint32_t start[128];
+    if (threadIdx.x < 128) start[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) atomicAdd(&start[cost_bucket(cost[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0u;
+        for (int b = 0; b < 128; b++) {
+            const uint32_t c = start[b];
+            start[b] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) order[atomicAdd(&start[cost_bucket(cost[i])], 1u)] = i;
+}
+
 __global__ void rand_init_kernel(uint32_t* state) {  // RandInit (Kernel.cu:160-164)
     if (threadIdx.x == 0 && blockIdx.x == 0) curand_init_state(1984ull, state);
 }
@@ -1522,6 +1589,7 @@ struct Variant {
     bool persistent = false;  // render_kernel_v4: device-filling grid + work queue
     bool half = false;        // binary16 child boxes (32-B nodes)
     int wpg = 1;              // v3/v4: independent waves per workgroup (block = 64 · wpg)
+    bool compact = false;     // v3: 13-word parking (needs spp < 8192, max_depth < 64, spp · max_depth < 8192)
 };
 
 // rt_set_variant(i) selects kVariants[i]
@@ -1542,6 +1610,10 @@ constexpr Variant kVariants[] = {
     // 24..27: v3 / v4 (64-B nodes) with 2 or 4 independent waves per workgroup
     {false, dev::STACK_LDS16, 1, 0, true, 128, false, false, 2}, {false, dev::STACK_LDS16, 1, 0, true, 256, false, false, 4},
     {false, dev::STACK_LDS16, 1, 0, true, 128, true, false, 2},  {false, dev::STACK_LDS16, 1, 0, true, 256, true, false, 4},
+    // 28: v3 × 4 waves/WG with binary16 nodes; 29: v3 × 4 waves/WG, ≤ 64 VGPRs (8 waves/SIMD by registers)
+    {false, dev::STACK_LDS16, 1, 0, true, 256, false, true, 4}, {false, dev::STACK_LDS16, 8, 0, true, 256, false, false, 4},
+    // 30, 31: 25 and 29 with compact parking (13 LDS words per lane)
+    {false, dev::STACK_LDS16, 1, 0, true, 256, false, false, 4, true}, {false, dev::STACK_LDS16, 8, 0, true, 256, false, false, 4, true},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -1550,10 +1622,10 @@ KernelFn pick_count(bool count) {
     return count ? dev::render_kernel<L, S, true, W> : dev::render_kernel<L, S, false, W>;
 }
 
-template <int W, int H = dev::NODES_48, int G = 1, bool PH = false>
+template <int W, int H = dev::NODES_48, int G = 1, bool PH = false, bool C = false>
 KernelFn v3_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v3<true, W, true, H, G, PH> : dev::render_kernel_v3<false, W, true, H, G, PH>;
-    return count ? dev::render_kernel_v3<true, W, false, H, G, PH> : dev::render_kernel_v3<false, W, false, H, G, PH>;
+    if (tex) return count ? dev::render_kernel_v3<true, W, true, H, G, PH, C> : dev::render_kernel_v3<false, W, true, H, G, PH, C>;
+    return count ? dev::render_kernel_v3<true, W, false, H, G, PH, C> : dev::render_kernel_v3<false, W, false, H, G, PH, C>;
 }
 
 template <int W, int H = dev::NODES_48, int G = 1, bool PH = false>
@@ -1606,11 +1678,70 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
     case 25: return v3_pick<1, dev::NODES_48, 4>(count, tex);
     case 26: return v4_pick<1, dev::NODES_64, 2>(count, tex);
     case 27: return v4_pick<1, dev::NODES_64, 4>(count, tex);
+    case 28: return v3_pick<1, dev::NODES_HALF, 4>(count, tex);
+    case 29: return v3_pick<8, dev::NODES_48, 4>(count, tex);
+    case 30: return v3_pick<1, dev::NODES_48, 4, false, true>(count, tex);
+    case 31: return v3_pick<8, dev::NODES_48, 4, false, true>(count, tex);
     default: return v4_pick<7, dev::NODES_64>(count, tex);
     }
 }
 
 thread_local int g_regen_threshold = 40;
+thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupancy experiments)
+thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
+thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
+thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
+
+// Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
+struct TilePlan {
+    uint32_t* cost = nullptr;
+    uint32_t* order = nullptr;
+    bool valid = false;  // an order has been planned (by an earlier launch on the same stream)
+};
+struct PlanKey {
+    int device;
+    void* stream;
+    uint32_t tiles_x, tiles;
+    bool operator<(const PlanKey& o) const {
+        if (device != o.device) return device < o.device;
+        if (stream != o.stream) return stream < o.stream;
+        if (tiles_x != o.tiles_x) return tiles_x < o.tiles_x;
+        return tiles < o.tiles;
+    }
+};
+std::map<PlanKey, TilePlan> g_plans;
+std::mutex g_plans_mu;
+constexpr size_t kMaxPlans = 32;
+
+int acquire_plan(const PlanKey& key, hipStream_t s, TilePlan** out) {
+    std::lock_guard<std::mutex> lock(g_plans_mu);
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) {
+        if (g_plans.size() >= kMaxPlans) {  // drop every plan (hipFree waits for the device)
+            for (auto& kv : g_plans) {
+                (void)hipFree(kv.second.cost);
+                (void)hipFree(kv.second.order);
+            }
+            g_plans.clear();
+        }
+        TilePlan p;
+        void* c = nullptr;
+        void* o = nullptr;
+        int rc = hip_check(hipMalloc(&c, (size_t)key.tiles * 4), "rt_render: tile cost allocation");
+        if (rc == RT_OK) rc = hip_check(hipMalloc(&o, (size_t)key.tiles * 4), "rt_render: tile order allocation");
+        if (rc == RT_OK) rc = hip_check(hipMemsetAsync(c, 0, (size_t)key.tiles * 4, s), "rt_render: tile cost reset");
+        if (rc != RT_OK) {
+            if (c) (void)hipFree(c);
+            if (o) (void)hipFree(o);
+            return rc;
+        }
+        p.cost = (uint32_t*)c;
+        p.order = (uint32_t*)o;
+        it = g_plans.emplace(key, p).first;
+    }
+    *out = &it->second;
+    return RT_OK;
+}
 thread_local int g_persistent_waves = 0;  // 0: occupancy query
 
 constexpr size_t kLdsLimit = 160 * 1024;
@@ -1661,6 +1792,16 @@ using namespace rt;
 
 extern "C" {
 
+int rt_set_wave_trace(void* buffer) {
+    g_wave_trace = (unsigned long long*)buffer;
+    return RT_OK;
+}
+
+int rt_set_tile_order(const void* order) {
+    g_tile_order = (const uint32_t*)order;
+    return RT_OK;
+}
+
 int rt_set_timing(int enabled) {
     g_timing = enabled != 0;
     return RT_OK;
@@ -1693,6 +1834,33 @@ int rt_set_tuning(int key, int value) {
         }
         int prev = g_leaf_max;
         g_leaf_max = value;
+        return prev;
+    }
+    if (key == RT_TUNE_SAH_TRAVERSAL) {
+        if (value < 1 || value > 1000) {
+            set_error("rt_set_tuning: SAH traversal cost (x10) must be in [1, 1000]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_sah_traversal_x10;
+        g_sah_traversal_x10 = value;
+        return prev;
+    }
+    if (key == RT_TUNE_ADAPTIVE_ORDER) {
+        if (value < 0 || value > 1) {
+            set_error("rt_set_tuning: adaptive order must be 0 or 1");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_adaptive_order;
+        g_adaptive_order = value;
+        return prev;
+    }
+    if (key == RT_TUNE_LDS_PAD) {
+        if (value < 0 || value > 65536 || value % 4) {
+            set_error("rt_set_tuning: LDS pad must be a multiple of 4 in [0, 65536]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_lds_pad;
+        g_lds_pad = value;
         return prev;
     }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
@@ -1768,6 +1936,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.rng_key_lo = (uint32_t)a->rng_seed;
     P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
     P.rng_frame = a->rng_frame;
+    P.wave_trace = g_wave_trace;
+    P.tile_order = g_tile_order;
     // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
     const rt_input_struct& in = a->inputs;
     P.width_f = (float)a->width;
@@ -1811,11 +1981,14 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // with four independent waves per workgroup for the many-sample frames (config 2: 64 spp, 25.7-26.2
     // vs 26.5-26.9 ms for one wave per workgroup, 27.4-27.8 ms for v4)
     if (variant < 0 || variant >= kNumVariants)
-        variant = (a->samples_per_pixel < 32 || a->max_depth > 8) ? 22 : 25;
+        variant = (a->samples_per_pixel < 32 || a->max_depth > 8) ? 22 : 13;
     if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
         variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
     if (kVariants[variant].half && !S.has_half_nodes)  // a plane beyond the binary16 range: f32 boxes
-        variant = variant == 18 ? 13 : (variant == 19 ? 16 : 17);
+        variant = variant == 18 ? 13 : (variant == 19 ? 16 : (variant == 28 ? 25 : 17));
+    if (kVariants[variant].compact &&
+        !(a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u))
+        variant = variant == 30 ? 25 : 29;  // the packed sample/depth/ray counters would overflow
     if (kVariants[variant].persistent && (a->samples_per_pixel == 0 || a->max_depth == 0))
         variant = kVariants[variant].half ? 18 : 13;  // the persistent kernel assumes every pixel traces a ray
     if (philox && !philox_capable(variant)) {
@@ -1833,7 +2006,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
     // v3/v4: per wave, the parked path state + a 16-bit stack of depth + 3 entries (two sentinel pads)
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
-                                  ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::PK_WORDS) * 64 * 4 + (size_t)(S.depth + 3) * 64 * 2
+                                  ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
+                                        (size_t)(S.depth + 3) * 64 * 2 +
+                                        (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
     size_t lds_bytes = (V.scene_lds ? scene_lds : 0) +
@@ -1863,6 +2038,16 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         rc = hip_check(hipMemsetAsync(P.work_counter, 0, sizeof(uint32_t), s), "rt_render: work queue reset");
         if (rc != RT_OK) return rc;
     }
+    P.num_tiles = tiles;
+    TilePlan* plan = nullptr;
+    if (V.stack == dev::STACK_LDS16 && !V.persistent && g_adaptive_order && !g_tile_order) {
+        int device = 0;
+        int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
+        if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles}, s, &plan);
+        if (rc != RT_OK) return rc;
+        P.tile_cost = plan->cost;
+        P.tile_order = plan->valid ? plan->order : nullptr;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing) {
         (void)hipEventCreate(&e0);
@@ -1872,6 +2057,12 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     (void)hipGetLastError();
     hipLaunchKernelGGL(fn, dim3(grid), dim3(V.block), lds_bytes, s, P);
     int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
+    if (rc == RT_OK && plan) {  // the next launch on this stream dispatches this frame's costliest tiles first
+        hipLaunchKernelGGL(dev::plan_order_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)plan->cost, plan->order,
+                           tiles);
+        rc = hip_check(hipGetLastError(), "rt_render: plan kernel launch", RT_ERR_LAUNCH);
+        if (rc == RT_OK) plan->valid = true;
+    }
     if (g_timing) {
         (void)hipEventRecord(e1, s);
         if (rc == RT_OK && hipEventSynchronize(e1) == hipSuccess) {

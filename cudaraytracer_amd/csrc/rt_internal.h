@@ -36,6 +36,7 @@ namespace rt {
 
 constexpr int kLeafMax = 4;         // max primitives per leaf (2-bit count in the leaf reference)
 extern thread_local int g_leaf_max;  // rt_set_tuning(RT_TUNE_LEAF_MAX): 1..kLeafMax, read by the BVH build
+extern thread_local int g_sah_traversal_x10;  // rt_set_tuning(RT_TUNE_SAH_TRAVERSAL): SAH node cost × 10
 constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) traversal stack
 
 struct HostScene {

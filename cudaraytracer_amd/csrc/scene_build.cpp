@@ -159,7 +159,7 @@ struct Builder {
         }
         Box all = range_box(b, e);
         float leaf_cost = all.area() * (float)n;
-        const float kTraversal = 1.2f;  // cost of one node visit relative to one primitive test
+        const float kTraversal = (float)g_sah_traversal_x10 / 10.0f;  // node visit cost / primitive test cost
         if (!must_split && n <= leaf_max && best_cost + kTraversal * all.area() >= leaf_cost) return make_leaf(b, e);
         std::stable_sort(order.begin() + b, order.begin() + e, [&](int x, int y) {
             return prims[x].centroid[best_axis] < prims[y].centroid[best_axis];
@@ -211,6 +211,7 @@ int check_texture(const rt_texture_desc& t, uint32_t num_images, std::string* er
 }  // namespace
 
 thread_local int g_leaf_max = kLeafMax;
+thread_local int g_sah_traversal_x10 = 12;
 
 int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images, std::vector<float>* out,
                    std::string* err) {

@@ -257,6 +257,14 @@ int rt_render(const rt_scene* scene, const rt_render_args* args, rt_stream strea
 int rt_set_timing(int enabled);
 float rt_last_kernel_ms(void);
 
+/* Diagnostic (per thread): device buffer of 2 × uint64 per wave that later v3 launches fill with each wave's
+ * start and end s_memrealtime (100 MHz) — occupancy/tail analysis (tools/wave_timeline.py).  NULL = off. */
+int rt_set_wave_trace(void* buffer);
+
+/* Experiment (per thread): device uint32 permutation of the frame's 8×8 tiles giving the v3 kernels' launch
+ * order (NULL = row-major).  Results do not depend on it (every pixel is independent); the time does. */
+int rt_set_tile_order(const void* order);
+
 /* Tuning/benchmark knob (per thread): -1 = automatic; 0..5 = (scene tables staged in LDS) * 3 + traversal
  * stack kind (0 = scratch, 1 = LDS, 2 = 4 VGPRs + scratch).  Returns the previous value. */
 int rt_set_variant(int variant);
@@ -267,7 +275,14 @@ int rt_set_variant(int variant);
 /*   RT_TUNE_LEAF_MAX: maximum primitives per BVH leaf used by later rt_scene_create calls (1..4, default 4). */
 /*   RT_TUNE_PERSISTENT_WAVES: waves per SIMD of the persistent kernels' grid (0 = occupancy query, default;
  *   1..16). */
-enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2 };
+/*   RT_TUNE_SAH_TRAVERSAL: cost of a node visit relative to a primitive test in the SAH leaf decision, ×10
+ *   (1..1000, default 12), used by later rt_scene_create calls. */
+/*   RT_TUNE_LDS_PAD: diagnostic, extra LDS bytes per wave of the v3/v4 kernels (occupancy experiments; 0).
+ *   RT_TUNE_ADAPTIVE_ORDER: 1 (default) = the v3 kernels dispatch a frame's tiles longest-first, ordered by
+ *   the per-tile wave lifetimes the previous launch on the same stream with the same tile grid measured;
+ *   0 = row-major.  The image does not depend on it. */
+enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
+                     RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5 };
 int rt_set_tuning(int key, int value);
 
 /* Host-side helpers (no device needed). */

@@ -23,7 +23,7 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = list(range(28))
+VARIANTS = list(range(32))
 # v3 (13), persistent v4 (16), binary16 nodes (18), persistent + binary16 (19)
 KEY_VARIANTS = [13, 16, 18, 19]
 
@@ -448,3 +448,29 @@ def test_philox_full_size_c2_rows_match_oracle():
     np.testing.assert_array_equal(r.image()[rows], ref[rows])
     rays = int(r.counters[0])
     assert 2.9 < rays / (cfg.width * cfg.height * cfg.spp) < 3.3
+
+
+def test_adaptive_tile_order_changes_schedule_not_pixels():
+    """The v3 kernels dispatch tiles longest-first by the previous launch's per-tile lifetimes
+    (RT_TUNE_ADAPTIVE_ORDER); frames rendered row-major, then reordered, are identical."""
+    cfg = scenes.CONFIGS["c2"].scaled(320, 176, 8)
+    ds = DeviceScene(scenes.builtin(cfg.scene))
+    lib().rt_set_variant(25)
+    prev = lib().rt_set_tuning(5, 0)
+    try:
+        r = Renderer(cfg.width, cfg.height)
+        r.render_init()
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
+        torch.cuda.synchronize()
+        row_major = r.image().copy()
+        lib().rt_set_tuning(5, 1)
+        for _ in range(3):  # the first launch records costs, the next ones dispatch longest-first
+            r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(r.image(), row_major)
+        st = po.init_states(cfg.width, cfg.height)
+        ref, _, _ = po.render(po.OracleScene(scenes.builtin(cfg.scene)), cfg.width, cfg.height, cfg.spp, cfg.depth,
+                              cfg.inputs(), st)
+        np.testing.assert_array_equal(row_major, ref)
+    finally:
+        lib().rt_set_tuning(5, prev if prev >= 0 else 1)

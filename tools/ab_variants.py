@@ -14,21 +14,26 @@ ap.add_argument("--spp", type=int, default=0)
 ap.add_argument("--thresholds", default="40", help="regen thresholds to try for resumable variants (>= 8)")
 ap.add_argument("--leafmax", default="4", help="BVH leaf sizes to try (RT_TUNE_LEAF_MAX)")
 ap.add_argument("--pwaves", default="0", help="persistent grid waves/SIMD to try (RT_TUNE_PERSISTENT_WAVES)")
+ap.add_argument("--sah", default="12", help="SAH traversal costs x10 to try (RT_TUNE_SAH_TRAVERSAL)")
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 if args.spp:
     cfg = cfg.scaled(cfg.width, cfg.height, args.spp)
 variants = []
-for lm in (int(x) for x in args.leafmax.split(",")):
-    for v in (int(v) for v in args.variants.split(",")):
-        for th in ([int(t) for t in args.thresholds.split(",")] if v >= 8 else [40]):
-            for pw in ([int(p) for p in args.pwaves.split(",")] if v in (16, 17, 19, 20) else [0]):
-                variants.append((v, th, lm, pw))
+for sah in (int(x) for x in args.sah.split(",")):
+    for lmv in (int(x) for x in args.leafmax.split(",")):
+        lm = (lmv, sah)
+        for v in (int(v) for v in args.variants.split(",")):
+            for th in ([int(t) for t in args.thresholds.split(",")] if v >= 8 else [40]):
+                for pw in ([int(p) for p in args.pwaves.split(",")] if v in (16, 17, 19, 20) else [0]):
+                    variants.append((v, th, lm, pw))
 scenes_by_lm = {}
 for lm in sorted({v[2] for v in variants}):
-    lib().rt_set_tuning(1, lm)
+    lib().rt_set_tuning(1, lm[0])
+    lib().rt_set_tuning(3, lm[1])
     scenes_by_lm[lm] = DeviceScene(scenes.builtin(cfg.scene))
 lib().rt_set_tuning(1, 4)
+lib().rt_set_tuning(3, 12)
 r = Renderer(cfg.width, cfg.height)
 r.render_init()
 inp = cfg.inputs()
@@ -55,4 +60,4 @@ for rnd in range(args.rounds):
         rays[v] = int(r.counters[0])
 for v in variants:
     med = statistics.median(times[v])
-    print(f"{args.config} variant {v[0]} thr {v[1]} leafmax {v[2]} pwaves {v[3]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)
+    print(f"{args.config} variant {v[0]} thr {v[1]} leafmax {v[2][0]} sah {v[2][1]} pwaves {v[3]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)

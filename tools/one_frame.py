@@ -11,9 +11,11 @@ ap.add_argument("--config", default="c2")
 ap.add_argument("--variant", type=int, default=-1)
 ap.add_argument("--frames", type=int, default=2)
 ap.add_argument("--rng", default="xorwow", choices=("xorwow", "philox"))
+ap.add_argument("--lds-pad", type=int, default=0)
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 lib().rt_set_variant(args.variant)
+lib().rt_set_tuning(4, args.lds_pad)
 ds = DeviceScene(scenes.builtin(cfg.scene))
 r = Renderer(cfg.width, cfg.height, rng=args.rng)
 r.render_init()
