@@ -11,6 +11,7 @@ from cudaraytracer_amd.renderer import DeviceScene, Renderer
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--variant", type=int, default=-1)
+ap.add_argument("--warm", action="store_true")
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 lib().rt_set_variant(args.variant)
@@ -19,6 +20,9 @@ r = Renderer(cfg.width, cfg.height)
 r.render_init()
 waves = ((cfg.width + 7) // 8) * ((cfg.height + 7) // 8)
 buf = torch.zeros(2 * waves + 64, dtype=torch.int64, device="cuda")
+if args.warm:  # one untraced frame first: the traced frame then runs in the adaptive (longest-first) order
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+    torch.cuda.synchronize()
 lib().rt_set_wave_trace(buf.data_ptr())
 r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
 torch.cuda.synchronize()
@@ -61,4 +65,4 @@ lib().rt_set_tile_order(order.data_ptr())
 ljf = timed()
 lib().rt_set_tile_order(None)
 base2 = timed()
-print(f"row-major {base:.2f} / {base2:.2f} ms, longest-first (previous frame's tile lifetimes) {ljf:.2f} ms")
+print(f"frames: {base:.2f} / {base2:.2f} ms (library's adaptive order), host-planned longest-first {ljf:.2f} ms")
