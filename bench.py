@@ -110,15 +110,20 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-philox-line", action="store_true", help="skip the secondary Philox-mode timing (N=1)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank renders on device 0 (use with --backend gloo)")
     args = ap.parse_args()
 
     rank, world, local_rank = parallel.env_rank()
     if world != args.gpus:
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    device = 0 if args.share_gpu else local_rank
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        parallel.init_process_group("nccl")
+        torch.cuda.set_device(device)
+        parallel.init_process_group(args.backend)
+    red_dev = torch.device("cpu") if args.backend == "gloo" else torch.device("cuda", device)
     cfg = scenes.CONFIGS[args.config]
     if world > 1:
         s = math.sqrt(world)
@@ -126,7 +131,7 @@ def main() -> None:
     lib().rt_set_variant(args.variant)
 
     band = parallel.DEFAULT_BAND_ROWS if world > 1 else cfg.height
-    r = Renderer(cfg.width, cfg.height, device=local_rank, band_rows=band, num_ranks=world, rank=rank, rng=args.rng)
+    r = Renderer(cfg.width, cfg.height, device=device, band_rows=band, num_ranks=world, rank=rank, rng=args.rng)
     scene = DeviceScene(scenes.builtin(cfg.scene))
     inputs = cfg.inputs()
     r.render_init()
@@ -167,8 +172,8 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     rays = int(r.counters[0].item())
-    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=r.device)
-    tot = torch.tensor([rays, f_launch], dtype=torch.int64, device=r.device)
+    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=red_dev)
+    tot = torch.tensor([rays, f_launch], dtype=torch.int64, device=red_dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)

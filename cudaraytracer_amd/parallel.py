@@ -9,6 +9,7 @@ followed by the inverse row permutation.  The reference has no multi-GPU path; t
 """
 from __future__ import annotations
 
+import functools
 import os
 
 import torch
@@ -32,25 +33,33 @@ def init_process_group(backend: str) -> None:
         dist.init_process_group(backend=backend)
 
 
+@functools.lru_cache(maxsize=64)
 def local_row_counts(height: int, band_rows: int, world: int) -> list[int]:
     return [len(band_rows_of(height, band_rows, world, r)) for r in range(world)]
 
 
+@functools.lru_cache(maxsize=64)
+def _rows_index(height: int, band_rows: int, world: int, rank: int, device: str) -> torch.Tensor:
+    return torch.tensor(band_rows_of(height, band_rows, world, rank), dtype=torch.long, device=device)
+
+
 def gather_bands(local: torch.Tensor, width: int, height: int, band_rows: int, dst: int = 0,
                  group=None) -> torch.Tensor | None:
-    """Gather every rank's (local_rows·W) framebuffer to `dst` and return the (H, W) image there."""
+    """Gather every rank's (local_rows·W) framebuffer to `dst` and return the (H, W) image there.  With
+    the gloo backend (CPU tests, single-GPU rehearsals) device buffers are staged through host memory."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     counts = local_row_counts(height, band_rows, world)
     max_rows = max(counts)
-    send = torch.zeros(max_rows * width, dtype=local.dtype, device=local.device)
-    send[: local.numel()] = local.reshape(-1)
+    via_host = local.is_cuda and dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if via_host else local.device
+    send = torch.zeros(max_rows * width, dtype=local.dtype, device=dev)
+    send[: local.numel()] = local.reshape(-1).to(dev)
     recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
     dist.gather(send, recv, dst=dst, group=group)
     if rank != dst:
         return None
-    full = torch.empty(height, width, dtype=local.dtype, device=local.device)
+    full = torch.empty(height, width, dtype=local.dtype, device=dev)
     for r in range(world):
-        rows = torch.tensor(band_rows_of(height, band_rows, world, r), dtype=torch.long, device=local.device)
-        full.index_copy_(0, rows, recv[r][: counts[r] * width].view(counts[r], width))
-    return full
+        full.index_copy_(0, _rows_index(height, band_rows, world, r, str(dev)), recv[r][: counts[r] * width].view(counts[r], width))
+    return full.to(local.device) if via_host else full
