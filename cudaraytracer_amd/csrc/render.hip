@@ -1114,6 +1114,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
     const f3 oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
+    const f3 pa = mk(invd.x < 0.0f ? 0.0f : invd.x, invd.y < 0.0f ? 0.0f : invd.y, invd.z < 0.0f ? 0.0f : invd.z);
+    const f3 pc = mk(invd.x < 0.0f ? invd.x : 0.0f, invd.y < 0.0f ? invd.y : 0.0f, invd.z < 0.0f ? invd.z : 0.0f);
     while (node != kSentinel16 || leaf < 0) {
         while ((uint32_t)node < (uint32_t)kSentinel16) {
             const int top1 = stk[(sp - 1u) * 64];
@@ -1150,16 +1152,41 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 ch0 = (int)(int16_t)(refs & 0xffffu);
                 ch1 = (int)refs >> 16;
             }
-            const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
-            const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
-            const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
-            const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
-            const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
-            const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
-            const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
-            const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
-            const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
-            const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+            float c0min, c0max, c1min, c1max;
+            if constexpr (NODES == NODES_HALF) {
+                const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
+                const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
+                const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
+                const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
+                const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
+                const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
+                c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+                c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+                c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+                c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+            } else {
+                // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0)
+                // for a positive direction component and (0, 1/d) for a negative one,
+                //   near = fma(lo, pa, fma(hi, pc, -o/d)),  far = fma(hi, pa, fma(lo, pc, -o/d))
+                // is fma(lo or hi, 1/d, -o/d) with one rounding — the value min/max of the two would pick —
+                // at four 2-cycle FMAs per axis instead of two FMAs, a min and a max.
+                const float nx0 = __builtin_fmaf(n0.x, pa.x, __builtin_fmaf(n0.y, pc.x, -oi.x));
+                const float fx0 = __builtin_fmaf(n0.y, pa.x, __builtin_fmaf(n0.x, pc.x, -oi.x));
+                const float ny0 = __builtin_fmaf(n0.z, pa.y, __builtin_fmaf(n0.w, pc.y, -oi.y));
+                const float fy0 = __builtin_fmaf(n0.w, pa.y, __builtin_fmaf(n0.z, pc.y, -oi.y));
+                const float nz0 = __builtin_fmaf(n2.x, pa.z, __builtin_fmaf(n2.y, pc.z, -oi.z));
+                const float fz0 = __builtin_fmaf(n2.y, pa.z, __builtin_fmaf(n2.x, pc.z, -oi.z));
+                const float nx1 = __builtin_fmaf(n1.x, pa.x, __builtin_fmaf(n1.y, pc.x, -oi.x));
+                const float fx1 = __builtin_fmaf(n1.y, pa.x, __builtin_fmaf(n1.x, pc.x, -oi.x));
+                const float ny1 = __builtin_fmaf(n1.z, pa.y, __builtin_fmaf(n1.w, pc.y, -oi.y));
+                const float fy1 = __builtin_fmaf(n1.w, pa.y, __builtin_fmaf(n1.z, pc.y, -oi.y));
+                const float nz1 = __builtin_fmaf(n2.z, pa.z, __builtin_fmaf(n2.w, pc.z, -oi.z));
+                const float fz1 = __builtin_fmaf(n2.w, pa.z, __builtin_fmaf(n2.z, pc.z, -oi.z));
+                c0min = fmaxf(fmaxf(nx0, ny0), fmaxf(nz0, kTmin));
+                c0max = fminf(fminf(fx0, fy0), fminf(fz0, t_best));
+                c1min = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, kTmin));
+                c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best));
+            }
             if (COUNT_TESTS) {
                 cnt.boxes += 2;
                 cnt.wnode += wave_leader();
