@@ -1098,6 +1098,28 @@ __device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col,
     }
 }
 
+// x / a correctly rounded from y = RN(1/a) (a one-off IEEE division per ray) in five 2-cycle ops instead
+// of the ~36-cycle div_scale/rcp/div_fmas/div_fixup sequence: two residual corrections, the last of which
+// is exact by Markstein's theorem once its input is within an ulp.  Valid for a in [2^-40, 2^40] and
+// |x| >= 2^-100 (smaller x give quotients the sphere test rejects either way); tools/check_fastdiv.c
+// checks 1e10 random and near-tie cases bit for bit against x / a.
+__device__ __forceinline__ float div_rn(const float x, const float a, const float y) {
+    const float q0 = x * y;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-a, q0, x), y, q0);
+    return __builtin_fmaf(__builtin_fmaf(-a, q1, x), y, q1);
+}
+
+// sqrtf(x) for x >= 2^-96 (finite or +inf): the instruction sequence LLVM emits for the correctly rounded
+// square root — v_sqrt_f32 and a residual check of its two neighbours — without the small-input scaling
+// and the 0/inf class test, neither of which changes the result in that range (saves ~24 of ~54 cycles).
+__device__ __forceinline__ float sqrt_rn(const float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+    r = __builtin_fmaf(-sup, s, x) > 0.0f ? sup : r;
+    return r;
+}
+
 // Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
 // until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
 // still tracing (the wave then shades the finished lanes and regenerates them).
@@ -1110,6 +1132,9 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     uint32_t sp = c.sp;
     float t_best = c.t_best;
     const float a_dd = dot(rd, rd);
+    // RN(1/a) for the sphere roots (div_rn); outside [2^-40, 2^40] the test divides the IEEE way
+    const float inv_a = 1.0f / a_dd;
+    const bool fast_div = a_dd >= 0x1p-40f && a_dd <= 0x1p40f;
     const f3 invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
@@ -1228,13 +1253,13 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     const float c = dot(oc, oc) - p1.x;
                     const float disc = b * b - a_dd * c;
                     if (disc > 0) {
-                        const float sq = sqrtf(disc);
-                        float t = (-b - sq) / a_dd;
+                        const float sq = disc >= 0x1p-96f ? sqrt_rn(disc) : sqrtf(disc);
+                        float t = fast_div ? div_rn(-b - sq, a_dd, inv_a) : (-b - sq) / a_dd;
                         if (t < t_best && t > kTmin) {
                             t_best = t;
                             hit = (int)i;
                         } else {
-                            t = (-b + sq) / a_dd;
+                            t = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
                             if (t < t_best && t > kTmin) {
                                 t_best = t;
                                 hit = (int)i;
