@@ -61,6 +61,31 @@ __device__ __forceinline__ f3 normalize(f3 v) {
     float inv = 1.0f / sqrtf(dot(v, v));
     return scale(inv, v);
 }
+// x / a correctly rounded from y = RN(1/a) (a one-off IEEE division) in five 2-cycle ops instead of the
+// ~36-cycle div_scale/rcp/div_fmas/div_fixup sequence: two residual corrections, the last of which is
+// exact by Markstein's theorem once its input is within an ulp.  Valid for |a| in [2^-40, 2^40] and
+// |x| >= 2^-100 or x == +0 (tools/check_fastdiv.c checks 1e10 random and near-tie cases bit for bit).
+__device__ __forceinline__ float div_rn(const float x, const float a, const float y) {
+    const float q0 = x * y;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-a, q0, x), y, q0);
+    return __builtin_fmaf(__builtin_fmaf(-a, q1, x), y, q1);
+}
+// divs(v, s) bit for bit, from y = RN(1/s) with |s| in [2^-40, 2^40] (y = 0 selects the IEEE division):
+// the fast path needs every |v_i / s| >= 2^-50 (so |v_i| >= 2^-90), anything else divides the IEEE way.
+__device__ __forceinline__ f3 divs_rn(const f3 v, const float s, const float y) {
+    const f3 q0 = mk(v.x * y, v.y * y, v.z * y);
+    if (fminf(fminf(fabsf(q0.x), fabsf(q0.y)), fabsf(q0.z)) >= 0x1p-50f) {
+        const float qx = __builtin_fmaf(__builtin_fmaf(-s, q0.x, v.x), y, q0.x);
+        const float qy = __builtin_fmaf(__builtin_fmaf(-s, q0.y, v.y), y, q0.y);
+        const float qz = __builtin_fmaf(__builtin_fmaf(-s, q0.z, v.z), y, q0.z);
+        return mk(__builtin_fmaf(__builtin_fmaf(-s, qx, v.x), y, qx), __builtin_fmaf(__builtin_fmaf(-s, qy, v.y), y, qy),
+                  __builtin_fmaf(__builtin_fmaf(-s, qz, v.z), y, qz));
+    }
+    return divs(v, s);
+}
+__device__ __forceinline__ float recip_in_range(const float s) {
+    return fabsf(s) >= 0x1p-40f && fabsf(s) <= 0x1p40f ? 1.0f / s : 0.0f;
+}
 __device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }
 __device__ __forceinline__ float clampf(float x, float a, float b) { return (x < a) ? a : ((x > b) ? b : x); }
 __device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
@@ -135,6 +160,7 @@ struct KParams {
     uint32_t grid_w, grid_h;  // pixels rendered: x < grid_w, global row < grid_h
     uint32_t rius_rtl;
     float width_f, cx, cy;
+    float inv_width;  // RN(1.0f / width_f) for div_rn
     float near_plane, far_plane;
     float origin[3], up[3], right[3];
     float fov_fwd[3];  // inputs.fov * forwardV           (Kernel.cu:142)
@@ -372,8 +398,9 @@ template <class PP, class R>
 __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& ro, f3& rd) {
     float xi1, xi2;
     draw2(rng, xi1, xi2);
-    const float u = (cam.xf + xi1) / P->width_f;
-    const float v = (cam.yf + xi2) / P->width_f;
+    // (x - cx + ξ) / width: the dividend is +0 or at least 2^-33 in magnitude (ξ in (0, 1]), inside div_rn's range
+    const float u = div_rn(cam.xf + xi1, P->width_f, P->inv_width);
+    const float v = div_rn(cam.yf + xi2, P->width_f, P->inv_width);
     const f3 dist = add(scale(u, cam.right), scale(v, cam.up));
     const f3 start = add(add(scale(P->near_plane, dist), cam.origin), cam.fov_fwd);
     const f3 second = add(add(scale(P->far_plane, dist), cam.k10_fwd), cam.origin);
@@ -395,14 +422,8 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         mtype = __float_as_uint(P->mats[3 * (tag >> 4)].x) & 15u;
     }
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
-    float len = 1.0f;
-    f3 ud = mk(0.0f, 0.0f, 0.0f);
-    if (hit < 0 || specular) {
-        len = length(rd);
-        ud.y = rd.y / len;
-    }
     if (hit < 0) {  // sky (Kernel.cu:41-44)
-        const float tt = 0.5f * (ud.y + 1.0f);
+        const float tt = 0.5f * (rd.y / length(rd) + 1.0f);
         const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
         contrib = mulv(att, c);
         return true;
@@ -417,7 +438,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
     float hu = 0.0f, hv = 0.0f;
     if (type == RT_SPHERE) {  // hit record of Sphere::Hit (Hittable.cuh:91-95)
         p = add(ro, scale(t, rd));
-        normal = divs(sub(p, xyz(p0)), p0.w);
+        normal = divs_rn(sub(p, xyz(p0)), p0.w, p1.y);  // p1.y = RN(1/radius) or 0 (scene_build.cpp)
         if (TEX && ttype == RT_IMAGE && mtype != RT_DIELECTRIC) {  // GetSphereUV (Hittable.cuh:119-125)
             const float theta = acosf(-normal.y);
             const float phi = atan2f(-normal.z, normal.x) + 3.141592654f;
@@ -449,9 +470,11 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         contrib = mulv(e, att);
         return true;
     }
+    float len = 1.0f;
+    f3 ud = mk(0.0f, 0.0f, 0.0f);
     if (specular) {
-        ud.x = rd.x / len;
-        ud.z = rd.z / len;
+        len = length(rd);
+        ud = divs_rn(rd, len, recip_in_range(len));
     }
     if (mtype == RT_DIELECTRIC) {  // Dielectric::Scatter (Material.cuh:106-136); attenuation (1,1,1)
         // Evaluated in an order that keeps few values live: every quantity is the same binary32 value the
@@ -1096,17 +1119,6 @@ __device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col,
         sample = park[PK_SAMPLE * 64];
         depth = park[PK_DEPTH * 64];
     }
-}
-
-// x / a correctly rounded from y = RN(1/a) (a one-off IEEE division per ray) in five 2-cycle ops instead
-// of the ~36-cycle div_scale/rcp/div_fmas/div_fixup sequence: two residual corrections, the last of which
-// is exact by Markstein's theorem once its input is within an ulp.  Valid for a in [2^-40, 2^40] and
-// |x| >= 2^-100 (smaller x give quotients the sphere test rejects either way); tools/check_fastdiv.c
-// checks 1e10 random and near-tie cases bit for bit against x / a.
-__device__ __forceinline__ float div_rn(const float x, const float a, const float y) {
-    const float q0 = x * y;
-    const float q1 = __builtin_fmaf(__builtin_fmaf(-a, q0, x), y, q0);
-    return __builtin_fmaf(__builtin_fmaf(-a, q1, x), y, q1);
 }
 
 // sqrtf(x) for x >= 2^-96 (finite or +inf): the instruction sequence LLVM emits for the correctly rounded
@@ -1993,6 +2005,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
     const rt_input_struct& in = a->inputs;
     P.width_f = (float)a->width;
+    P.inv_width = 1.0f / P.width_f;
     P.cx = (float)a->width / 2.0f;
     P.cy = (float)a->height / 2.0f;
     P.near_plane = in.near_plane;

@@ -369,7 +369,9 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         uint32_t tag = (uint32_t)h.type | ((uint32_t)h.material << 4);
         if (h.type == RT_SPHERE) {
             o[0] = h.center[0]; o[1] = h.center[1]; o[2] = h.center[2]; o[3] = h.radius;
-            o[4] = h.radius * h.radius; o[5] = 0.0f; o[6] = 0.0f;
+            // o[5]: RN(1/radius) for the kernel's fast normal division (render.hip divs_rn), 0 = IEEE division
+            const float ar = std::fabs(h.radius);
+            o[4] = h.radius * h.radius; o[5] = (ar >= 0x1p-40f && ar <= 0x1p40f) ? 1.0f / h.radius : 0.0f; o[6] = 0.0f;
         } else {
             RectGeom g = rect_geom(h);
             o[0] = g.k; o[1] = g.a0; o[2] = g.a1; o[3] = g.b0;
