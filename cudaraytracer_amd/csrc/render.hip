@@ -1140,7 +1140,10 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                                             const float4* __restrict__ prims, int16_t* const stk,
                                             const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
                                             Counts& cnt) {
-    int node = c.node, leaf = c.leaf, hit = c.hit;
+    // node / leaf references as unsigned 16-bit values: internal nodes < 0x7fff, kSentinel16 = 0x7fff, leaf
+    // references (int16 < 0 in the layout) >= 0x8000; leaf == 0: no postponed leaf
+    uint32_t node = (uint32_t)c.node, leaf = (uint32_t)c.leaf;
+    int hit = c.hit;
     uint32_t sp = c.sp;
     float t_best = c.t_best;
     const float a_dd = dot(rd, rd);
@@ -1153,12 +1156,13 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     const f3 oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
     const f3 pa = mk(invd.x < 0.0f ? 0.0f : invd.x, invd.y < 0.0f ? 0.0f : invd.y, invd.z < 0.0f ? 0.0f : invd.z);
     const f3 pc = mk(invd.x < 0.0f ? invd.x : 0.0f, invd.y < 0.0f ? invd.y : 0.0f, invd.z < 0.0f ? invd.z : 0.0f);
-    while (node != kSentinel16 || leaf < 0) {
-        while ((uint32_t)node < (uint32_t)kSentinel16) {
-            const int top1 = stk[(sp - 1u) * 64];
-            const int top2 = stk[(sp - 2u) * 64];
+    const uint16_t* ustk = (const uint16_t*)stk;
+    while (node != (uint32_t)kSentinel16 || leaf >= 0x8000u) {
+        while (node < (uint32_t)kSentinel16) {
+            const uint32_t top1 = ustk[(sp - 1u) * 64];
+            const uint32_t top2 = ustk[(sp - 2u) * 64];
             float4 n0, n1, n2;
-            int ch0, ch1;
+            uint32_t ch0, ch1;
             if constexpr (NODES == NODES_HALF) {  // 32-B node: binary16 planes (exact in f32: v_fma_mix_f32) + refs
                 const uint32_t noff = (uint32_t)node << 5;
                 const uint4 q0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
@@ -1169,16 +1173,16 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 n0 = make_float4((float)h0.x, (float)h0.y, (float)h1.x, (float)h1.y);
                 n1 = make_float4((float)h2.x, (float)h2.y, (float)h3.x, (float)h3.y);
                 n2 = make_float4((float)h4.x, (float)h4.y, (float)h5.x, (float)h5.y);
-                ch0 = (int)(int16_t)(q1.z & 0xffffu);
-                ch1 = (int)q1.z >> 16;
+                ch0 = q1.z & 0xffffu;
+                ch1 = q1.z >> 16;
             } else if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
                 const uint32_t noff = (uint32_t)node << 6;
                 n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
                 n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
                 n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
                 const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
-                ch0 = (int)r2.x;
-                ch1 = (int)r2.y;
+                ch0 = r2.x & 0xffffu;
+                ch1 = r2.y & 0xffffu;
             } else {  // 48 B of f32 boxes + 4 B of references
                 uint32_t noff;  // node · 48 with the full-rate 24-bit multiply (LLVM otherwise emits v_mul_lo_u32)
                 asm("v_mul_u32_u24 %0, 48, %1" : "=v"(noff) : "v"(node));
@@ -1186,8 +1190,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
                 n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
                 const uint32_t refs = __builtin_amdgcn_raw_buffer_load_b32(rrsrc, (uint32_t)node * 4u, 0, 0);
-                ch0 = (int)(int16_t)(refs & 0xffffu);
-                ch1 = (int)refs >> 16;
+                ch0 = refs & 0xffffu;
+                ch1 = refs >> 16;
             }
             float c0min, c0max, c1min, c1max;
             if constexpr (NODES == NODES_HALF) {
@@ -1232,24 +1236,26 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             const bool h1 = c1min <= c1max;
             const bool both = h0 && h1, none = !(h0 || h1);
             const bool swap = c1min < c0min;
-            const int nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
-            const int farc = swap ? ch0 : ch1;
+            const uint32_t nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
+            const uint32_t farc = swap ? ch0 : ch1;
             stk[sp * 64] = (int16_t)farc;
-            int nxt = none ? top1 : nearc;
-            uint32_t nsp = sp + (both ? 1u : 0u) - ((none && sp > kStackBase) ? 1u : 0u);
+            uint32_t nxt = none ? top1 : nearc;
+            // no underflow guards: the two sentinel pads below kStackBase make a pop of the empty stack
+            // yield kSentinel16, which ends this lane's traversal before sp can drop further
+            uint32_t nsp = sp + (both ? 1u : 0u) - (none ? 1u : 0u);
             // first leaf: postpone it and pop the next entry (the stack top after this visit)
-            const bool postpone = nxt < 0 && leaf == 0;
-            const int after_top = both ? farc : (none ? top2 : top1);
+            const bool postpone = nxt >= 0x8000u && leaf == 0;
+            const uint32_t after_top = both ? farc : (none ? top2 : top1);
             leaf = postpone ? nxt : leaf;
             nxt = postpone ? after_top : nxt;
-            nsp = (postpone && nsp > kStackBase) ? nsp - 1u : nsp;
+            nsp = postpone ? nsp - 1u : nsp;
             node = nxt;
             sp = nsp;
             if (__ballot(leaf == 0) == 0) break;
         }
         const uint64_t t_leaf = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
-        while (leaf < 0) {
-            const uint32_t l = ~(uint32_t)leaf;
+        while (leaf >= 0x8000u) {
+            const uint32_t l = leaf ^ 0xffffu;
             const uint32_t first = l >> 2, count = (l & 3u) + 1u;
             for (uint32_t i = first; i < first + count; i++) {
                 const float4 p0 = prims[2 * i + 0];
@@ -1295,17 +1301,17 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 }
             }
             leaf = 0;
-            if (node < 0) {
+            if (node >= 0x8000u) {
                 leaf = node;
-                node = stk[(sp - 1u) * 64];
-                sp = sp > kStackBase ? sp - 1u : kStackBase;
+                node = ustk[(sp - 1u) * 64];
+                sp--;
             }
         }
         if (COUNT_TESTS) cnt.cleaf += __builtin_amdgcn_s_memtime() - t_leaf;
         if ((uint32_t)__popcll(__ballot(1)) < threshold) break;
     }
-    c.node = node;
-    c.leaf = leaf;
+    c.node = (int)node;
+    c.leaf = (int)leaf;
     c.hit = hit;
     c.sp = sp;
     c.t_best = t_best;
