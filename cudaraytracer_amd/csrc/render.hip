@@ -229,6 +229,7 @@ template <> struct StackOf<STACK_HYBRID> { using T = HybridStack; };
 struct Counts {
     uint32_t rays, boxes, prims, primary;
     uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
+    uint32_t wnode_uniform = 0, wleaf_uniform = 0;  // COUNT_TESTS (v3): ... of them with one node / primitive
     uint64_t ctrav = 0, cshade = 0, ctotal = 0, cleaf = 0;  // COUNT_TESTS (v3): wave clock cycles per phase
 };
 
@@ -422,6 +423,9 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         mtype = __float_as_uint(P->mats[3 * (tag >> 4)].x) & 15u;
     }
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
+#ifdef RT_PAD_SHADE
+    for (int pad = 0; pad < RT_PAD_SHADE; pad++) asm volatile("v_mov_b32 %0, %0" : "+v"(t));
+#endif
     if (hit < 0) {  // sky (Kernel.cu:41-44)
         const float tt = 0.5f * (rd.y / length(rd) + 1.0f);
         const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
@@ -573,6 +577,8 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt
             atomicAdd(&P.counters[4], (unsigned long long)cnt.wnode);
             atomicAdd(&P.counters[5], (unsigned long long)cnt.wleaf);
             atomicAdd(&P.counters[6], (unsigned long long)cnt.wshade);
+            atomicAdd(&P.counters[11], (unsigned long long)cnt.wnode_uniform);
+            atomicAdd(&P.counters[12], (unsigned long long)cnt.wleaf_uniform);
             if (cnt.ctotal && wave_leader()) {  // one lane per wave: the stamps are wave-uniform
                 atomicAdd(&P.counters[7], (unsigned long long)cnt.ctrav);
                 atomicAdd(&P.counters[8], (unsigned long long)cnt.cshade);
@@ -1132,11 +1138,22 @@ __device__ __forceinline__ float sqrt_rn(const float x) {
     return r;
 }
 
+// Constant-address-space views of the read-only scene buffers: loads from them at wave-uniform indices become
+// scalar loads (s_load_dword*) whose results feed VALU instructions as SGPR operands.
+typedef const __attribute__((address_space(4))) float ConstF32;
+typedef const __attribute__((address_space(4))) uint32_t ConstU32;
+typedef const __attribute__((address_space(4))) uint8_t ConstU8;
+#ifndef RT_SCALAR_NODES
+#define RT_SCALAR_NODES 1
+#endif
+constexpr bool kScalarNodes = RT_SCALAR_NODES != 0;
+
 // Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
 // until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
 // still tracing (the wave then shades the finished lanes and regenerates them).
 template <bool COUNT_TESTS, int NODES>
 __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, const __amdgpu_buffer_rsrc_t rrsrc,
+                                            const float4* __restrict__ nodes48, const uint32_t* __restrict__ refs16,
                                             const float4* __restrict__ prims, int16_t* const stk,
                                             const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
                                             Counts& cnt) {
@@ -1161,56 +1178,14 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         while (node < (uint32_t)kSentinel16) {
             const uint32_t top1 = ustk[(sp - 1u) * 64];
             const uint32_t top2 = ustk[(sp - 2u) * 64];
-            float4 n0, n1, n2;
-            uint32_t ch0, ch1;
-            if constexpr (NODES == NODES_HALF) {  // 32-B node: binary16 planes (exact in f32: v_fma_mix_f32) + refs
-                const uint32_t noff = (uint32_t)node << 5;
-                const uint4 q0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
-                const uint4 q1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
-                const half2v h0 = __builtin_bit_cast(half2v, q0.x), h1 = __builtin_bit_cast(half2v, q0.y);
-                const half2v h2 = __builtin_bit_cast(half2v, q0.z), h3 = __builtin_bit_cast(half2v, q0.w);
-                const half2v h4 = __builtin_bit_cast(half2v, q1.x), h5 = __builtin_bit_cast(half2v, q1.y);
-                n0 = make_float4((float)h0.x, (float)h0.y, (float)h1.x, (float)h1.y);
-                n1 = make_float4((float)h2.x, (float)h2.y, (float)h3.x, (float)h3.y);
-                n2 = make_float4((float)h4.x, (float)h4.y, (float)h5.x, (float)h5.y);
-                ch0 = q1.z & 0xffffu;
-                ch1 = q1.z >> 16;
-            } else if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
-                const uint32_t noff = (uint32_t)node << 6;
-                n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
-                n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
-                n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
-                const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
-                ch0 = r2.x & 0xffffu;
-                ch1 = r2.y & 0xffffu;
-            } else {  // 48 B of f32 boxes + 4 B of references
-                uint32_t noff;  // node · 48 with the full-rate 24-bit multiply (LLVM otherwise emits v_mul_lo_u32)
-                asm("v_mul_u32_u24 %0, 48, %1" : "=v"(noff) : "v"(node));
-                n0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
-                n1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
-                n2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0));
-                const uint32_t refs = __builtin_amdgcn_raw_buffer_load_b32(rrsrc, (uint32_t)node * 4u, 0, 0);
-                ch0 = refs & 0xffffu;
-                ch1 = refs >> 16;
-            }
             float c0min, c0max, c1min, c1max;
-            if constexpr (NODES == NODES_HALF) {
-                const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
-                const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
-                const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
-                const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
-                const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
-                const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
-                c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
-                c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
-                c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
-                c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
-            } else {
-                // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0)
-                // for a positive direction component and (0, 1/d) for a negative one,
-                //   near = fma(lo, pa, fma(hi, pc, -o/d)),  far = fma(hi, pa, fma(lo, pc, -o/d))
-                // is fma(lo or hi, 1/d, -o/d) with one rounding — the value min/max of the two would pick —
-                // at four 2-cycle FMAs per axis instead of two FMAs, a min and a max.
+            uint32_t ch0, ch1;
+            // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0) for a
+            // positive direction component and (0, 1/d) for a negative one,
+            //   near = fma(lo, pa, fma(hi, pc, -o/d)),  far = fma(hi, pa, fma(lo, pc, -o/d))
+            // is fma(lo or hi, 1/d, -o/d) with one rounding — the value min/max of the two would pick — at four
+            // 2-cycle FMAs per axis instead of two FMAs, a min and a max.
+            const auto slab = [&](const float4 n0, const float4 n1, const float4 n2) {
                 const float nx0 = __builtin_fmaf(n0.x, pa.x, __builtin_fmaf(n0.y, pc.x, -oi.x));
                 const float fx0 = __builtin_fmaf(n0.y, pa.x, __builtin_fmaf(n0.x, pc.x, -oi.x));
                 const float ny0 = __builtin_fmaf(n0.z, pa.y, __builtin_fmaf(n0.w, pc.y, -oi.y));
@@ -1227,10 +1202,66 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 c0max = fminf(fminf(fx0, fy0), fminf(fz0, t_best));
                 c1min = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, kTmin));
                 c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best));
+            };
+            if constexpr (NODES == NODES_HALF) {  // 32-B node: binary16 planes (exact in f32: v_fma_mix_f32) + refs
+                const uint32_t noff = (uint32_t)node << 5;
+                const uint4 q0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
+                const uint4 q1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
+                const half2v h0 = __builtin_bit_cast(half2v, q0.x), h1 = __builtin_bit_cast(half2v, q0.y);
+                const half2v h2 = __builtin_bit_cast(half2v, q0.z), h3 = __builtin_bit_cast(half2v, q0.w);
+                const half2v h4 = __builtin_bit_cast(half2v, q1.x), h5 = __builtin_bit_cast(half2v, q1.y);
+                const float4 n0 = make_float4((float)h0.x, (float)h0.y, (float)h1.x, (float)h1.y);
+                const float4 n1 = make_float4((float)h2.x, (float)h2.y, (float)h3.x, (float)h3.y);
+                const float4 n2 = make_float4((float)h4.x, (float)h4.y, (float)h5.x, (float)h5.y);
+                ch0 = q1.z & 0xffffu;
+                ch1 = q1.z >> 16;
+                const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
+                const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
+                const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
+                const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
+                const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
+                const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
+                c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+                c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+                c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+                c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+            } else if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
+                const uint32_t noff = (uint32_t)node << 6;
+                const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
+                ch0 = r2.x & 0xffffu;
+                ch1 = r2.y & 0xffffu;
+                slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
+                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
+                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
+            } else {  // 48 B of f32 boxes + 4 B of references
+                const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
+                if (kScalarNodes && __ballot(node != nu) == 0) {
+                    // every active lane visits the same node: scalar loads through the constant cache, planes as
+                    // SGPR operands of the FMAs — no vector-memory (TA/TD) traffic, the kernel's busiest unit
+                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes48 + nu * 48u);
+                    const uint32_t refs = *(const ConstU32*)((const ConstU8*)refs16 + nu * 4u);
+                    ch0 = refs & 0xffffu;
+                    ch1 = refs >> 16;
+                    slab(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
+                         make_float4(cn[8], cn[9], cn[10], cn[11]));
+                } else {
+                    uint32_t noff;  // node · 48 with the full-rate 24-bit multiply (LLVM otherwise emits v_mul_lo_u32)
+                    asm("v_mul_u32_u24 %0, 48, %1" : "=v"(noff) : "v"(node));
+                    const uint32_t refs = __builtin_amdgcn_raw_buffer_load_b32(rrsrc, (uint32_t)node * 4u, 0, 0);
+                    ch0 = refs & 0xffffu;
+                    ch1 = refs >> 16;
+                    slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
+                }
             }
+#ifdef RT_PAD_NODE  // sensitivity experiment: RT_PAD_NODE extra 2-cycle VALU ops per node visit
+            for (int pad = 0; pad < RT_PAD_NODE; pad++) asm volatile("v_mov_b32 %0, %0" : "+v"(c0min));
+#endif
             if (COUNT_TESTS) {
                 cnt.boxes += 2;
                 cnt.wnode += wave_leader();
+                if (__ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0) cnt.wnode_uniform += wave_leader();
             }
             const bool h0 = c0min <= c0max;
             const bool h1 = c1min <= c1max;
@@ -1261,9 +1292,14 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 const float4 p0 = prims[2 * i + 0];
                 const float4 p1 = prims[2 * i + 1];
                 const uint32_t type = __float_as_uint(p1.w) & 15u;
+#ifdef RT_PAD_LEAF
+                float padv = p0.x;
+                for (int pad = 0; pad < RT_PAD_LEAF; pad++) asm volatile("v_mov_b32 %0, %0" : "+v"(padv));
+#endif
                 if (COUNT_TESTS) {
                     cnt.prims++;
                     cnt.wleaf += wave_leader();
+                    if (__ballot(i != (uint32_t)__builtin_amdgcn_readfirstlane(i)) == 0) cnt.wleaf_uniform += wave_leader();
                 }
                 if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
                     const f3 oc = sub(ro, xyz(p0));
@@ -1371,7 +1407,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
     while (true) {
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, prims, stk, threshold, ro, rd, c, cnt);
+            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -1475,7 +1511,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(con
     const uint32_t threshold = P.regen_threshold;
 
     while (true) {
-        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, prims, stk, threshold, ro, rd, c, cnt);
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
         uint32_t sample, depth, rays;
@@ -1684,6 +1720,8 @@ constexpr Variant kVariants[] = {
     {false, dev::STACK_LDS16, 1, 0, true, 256, false, true, 4}, {false, dev::STACK_LDS16, 8, 0, true, 256, false, false, 4},
     // 30, 31: 25 and 29 with compact parking (13 LDS words per lane)
     {false, dev::STACK_LDS16, 1, 0, true, 256, false, false, 4, true}, {false, dev::STACK_LDS16, 8, 0, true, 256, false, false, 4, true},
+    // 32, 33: 13 (one wave per workgroup) with compact parking, ≤ 64 VGPRs (32) or the compiler's choice (33)
+    {false, dev::STACK_LDS16, 8, 0, true, 64, false, false, 1, true}, {false, dev::STACK_LDS16, 1, 0, true, 64, false, false, 1, true},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -1752,6 +1790,8 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
     case 29: return v3_pick<8, dev::NODES_48, 4>(count, tex);
     case 30: return v3_pick<1, dev::NODES_48, 4, false, true>(count, tex);
     case 31: return v3_pick<8, dev::NODES_48, 4, false, true>(count, tex);
+    case 32: return v3_pick<8, dev::NODES_48, 1, false, true>(count, tex);
+    case 33: return v3_pick<1, dev::NODES_48, 1, false, true>(count, tex);
     default: return v4_pick<7, dev::NODES_64>(count, tex);
     }
 }
@@ -2059,7 +2099,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         variant = variant == 18 ? 13 : (variant == 19 ? 16 : (variant == 28 ? 25 : 17));
     if (kVariants[variant].compact &&
         !(a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u))
-        variant = variant == 30 ? 25 : 29;  // the packed sample/depth/ray counters would overflow
+        variant = variant == 30 ? 25 : (variant == 31 ? 29 : (variant == 32 ? 15 : 13));  // packed counters would overflow
     if (kVariants[variant].persistent && (a->samples_per_pixel == 0 || a->max_depth == 0))
         variant = kVariants[variant].half ? 18 : 13;  // the persistent kernel assumes every pixel traces a ray
     if (philox && !philox_capable(variant)) {

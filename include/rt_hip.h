@@ -235,7 +235,9 @@ typedef struct rt_render_args {
     uint64_t* counters;       /* optional device uint64[16]: rays, box tests, primitive tests, primary samples;
                                  with RT_FLAG_COUNT_TESTS also [4..6] = wave-level iterations of node visits,
                                  primitive tests and shading (SIMD-efficiency diagnostics) and, for the v3
-                                 kernels, [7..9] = wave clock cycles spent tracing, shading, in total */
+                                 kernels, [7..10] = wave clock cycles spent tracing, shading, in total and
+                                 in leaves, [11..12] = node / primitive wave-iterations whose active lanes
+                                 all test the same node / primitive */
     uint32_t width;
     uint32_t height;          /* global image height */
     uint32_t samples_per_pixel;

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Build librt_hip.so with extra compile definitions into <out.so> (A/B experiments on the GPU box).
+#   bash tools/build_variant_lib.sh <out.so> [-DNAME=VALUE ...]
+set -eu
+OUT=$(realpath -m "$1"); shift
+cd "$(dirname "$0")/../cudaraytracer_amd/csrc"
+T=$(mktemp -d)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-slp-vectorize -mllvm -simplifycfg-sink-common=false "$@" -c render.hip -o $T/render.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" $T/render.o ../../build/obj/api.o ../../build/obj/scene_build.o ../../build/obj/builtin_scenes.o
+rm -rf $T
