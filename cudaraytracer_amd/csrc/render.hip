@@ -1285,10 +1285,18 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             if (__ballot(leaf == 0) == 0) break;
         }
         const uint64_t t_leaf = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
-        while (leaf >= 0x8000u) {
+        // One primitive per lane per iteration: a lane walks its leaf's primitives and then the leaves
+        // that follow on its stack with its own cursor, so lanes with short leaves do not wait for the
+        // wave's longest leaf (same primitives in the same order per lane as a per-leaf loop).
+        uint32_t cur = 0u, end = 0u;
+        if (leaf >= 0x8000u) {
             const uint32_t l = leaf ^ 0xffffu;
-            const uint32_t first = l >> 2, count = (l & 3u) + 1u;
-            for (uint32_t i = first; i < first + count; i++) {
+            cur = l >> 2;
+            end = cur + (l & 3u) + 1u;
+        }
+        while (cur < end) {
+            {
+                const uint32_t i = cur;
                 const float4 p0 = prims[2 * i + 0];
                 const float4 p1 = prims[2 * i + 1];
                 const uint32_t type = __float_as_uint(p1.w) & 15u;
@@ -1336,11 +1344,16 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     }
                 }
             }
-            leaf = 0;
-            if (node >= 0x8000u) {
-                leaf = node;
-                node = ustk[(sp - 1u) * 64];
-                sp--;
+            if (++cur == end) {
+                leaf = 0;
+                if (node >= 0x8000u) {
+                    leaf = node;
+                    const uint32_t l = leaf ^ 0xffffu;
+                    cur = l >> 2;
+                    end = cur + (l & 3u) + 1u;
+                    node = ustk[(sp - 1u) * 64];
+                    sp--;
+                }
             }
         }
         if (COUNT_TESTS) cnt.cleaf += __builtin_amdgcn_s_memtime() - t_leaf;
