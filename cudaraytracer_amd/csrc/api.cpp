@@ -38,7 +38,8 @@ static void free_device(DeviceScene* s) {
     if (s->nodes48) (void)hipFree((void*)s->nodes48);
     if (s->refs16) (void)hipFree((void*)s->refs16);
     if (s->nodes32) (void)hipFree((void*)s->nodes32);
-    s->nodes48 = s->refs16 = s->nodes32 = nullptr;
+    if (s->nodes_w4) (void)hipFree((void*)s->nodes_w4);
+    s->nodes48 = s->refs16 = s->nodes32 = s->nodes_w4 = nullptr;
     if (s->prims) (void)hipFree((void*)s->prims);
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);
@@ -62,6 +63,11 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     d.refs16 = p;
     if ((rc = upload(h.nodes32, &p, "hipMalloc/hipMemcpy(nodes32)"))) goto fail;
     d.nodes32 = p;
+    if ((rc = upload(h.nodes_w4, &p, "hipMalloc/hipMemcpy(nodes_w4)"))) goto fail;
+    d.nodes_w4 = p;
+    d.num_nodes_w4 = h.num_nodes_w4;
+    d.depth_w4 = h.depth_w4;
+    d.stack_w4 = h.stack_w4;
     if ((rc = upload(h.prims, &p, "hipMalloc/hipMemcpy(prims)"))) goto fail;
     d.prims = p;
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;

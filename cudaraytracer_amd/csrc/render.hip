@@ -46,7 +46,7 @@ typedef __fp16 half2v __attribute__((ext_vector_type(2)));
 typedef float fl2 __attribute__((ext_vector_type(2)));
 
 // BVH node layouts read by the v3/v4 traversal (template argument NODES)
-enum NodeLayout { NODES_48 = 0, NODES_HALF = 1, NODES_64 = 2 };
+enum NodeLayout { NODES_48 = 0, NODES_HALF = 1, NODES_64 = 2, NODES_W4 = 3 };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -143,6 +143,8 @@ struct KParams {
     const float4* nodes;
     const float4* nodes48;   // v3: three box float4 per node
     const uint32_t* refs16;  // v3: packed 16-bit child references
+    const float* nodes_w4;   // v3 NODES_W4: 26 words per 4-wide node (scene_build.cpp collapse_w4)
+    uint32_t num_nodes_w4;
     const uint32_t* nodes32; // v3/v4 HALF: 32-B nodes with binary16 child boxes
     const float4* prims;
     const float4* mats;
@@ -1178,6 +1180,79 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         while (node < (uint32_t)kSentinel16) {
             const uint32_t top1 = ustk[(sp - 1u) * 64];
             const uint32_t top2 = ustk[(sp - 2u) * 64];
+            if constexpr (NODES == NODES_W4) {
+                // 4-wide node: one key per child, (bits of its entry distance, upper 16) | reference for a hit
+                // and +inf | reference for a miss (entry distances are >= kTmin > 0, so the bits order like
+                // the floats); a 5-exchange network sorts them, the nearest hit is visited next and the other
+                // hits go onto the stack farthest first.  Truncating the distance only reorders near-ties.
+                uint32_t k0, k1, k2, k3;
+                const auto keys = [&](const float4 a, const float4 b, const float4 cq, const float4 d, const float4 e,
+                                      const float4 f, const uint32_t r01, const uint32_t r23) {
+                    const auto key = [&](float lx, float hx, float ly, float hy, float lz, float hz, uint32_t ref) {
+                        const float nx = __builtin_fmaf(lx, pa.x, __builtin_fmaf(hx, pc.x, -oi.x));
+                        const float fx = __builtin_fmaf(hx, pa.x, __builtin_fmaf(lx, pc.x, -oi.x));
+                        const float ny = __builtin_fmaf(ly, pa.y, __builtin_fmaf(hy, pc.y, -oi.y));
+                        const float fy = __builtin_fmaf(hy, pa.y, __builtin_fmaf(ly, pc.y, -oi.y));
+                        const float nz = __builtin_fmaf(lz, pa.z, __builtin_fmaf(hz, pc.z, -oi.z));
+                        const float fz = __builtin_fmaf(hz, pa.z, __builtin_fmaf(lz, pc.z, -oi.z));
+                        const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, kTmin));
+                        const float tf = fminf(fminf(fx, fy), fminf(fz, t_best));
+                        return tn <= tf ? ((__float_as_uint(tn) & 0xffff0000u) | ref) : (0x7f800000u | ref);
+                    };
+                    k0 = key(a.x, a.y, a.z, a.w, b.x, b.y, r01 & 0xffffu);
+                    k1 = key(b.z, b.w, cq.x, cq.y, cq.z, cq.w, r01 >> 16);
+                    k2 = key(d.x, d.y, d.z, d.w, e.x, e.y, r23 & 0xffffu);
+                    k3 = key(e.z, e.w, f.x, f.y, f.z, f.w, r23 >> 16);
+                };
+                const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
+                if (kScalarNodes && __ballot(node != nu) == 0) {
+                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes48 + nu * 104u);
+                    const ConstU32* cr = (const ConstU32*)((const ConstU8*)nodes48 + nu * 104u + 96u);
+                    keys(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
+                         make_float4(cn[8], cn[9], cn[10], cn[11]), make_float4(cn[12], cn[13], cn[14], cn[15]),
+                         make_float4(cn[16], cn[17], cn[18], cn[19]), make_float4(cn[20], cn[21], cn[22], cn[23]),
+                         cr[0], cr[1]);
+                } else {
+                    uint32_t noff;  // node · 104 with the full-rate 24-bit multiply
+                    asm("v_mul_u32_u24 %0, 0x68, %1" : "=v"(noff) : "v"(node));
+                    const uint2 rr = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 96u, 0, 0));
+                    keys(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 48u, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 64u, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 80u, 0, 0)),
+                         rr.x, rr.y);
+                }
+                const uint32_t a0 = min(k0, k1), a1 = max(k0, k1), b0 = min(k2, k3), b1 = max(k2, k3);
+                const uint32_t s0 = min(a0, b0), m1 = max(a0, b0), m2 = min(a1, b1), s3 = max(a1, b1);
+                const uint32_t s1 = min(m1, m2), s2 = max(m1, m2);
+                const uint32_t nhit = (s0 < 0x7f800000u ? 1u : 0u) + (s1 < 0x7f800000u ? 1u : 0u) +
+                                     (s2 < 0x7f800000u ? 1u : 0u) + (s3 < 0x7f800000u ? 1u : 0u);
+                if (COUNT_TESTS) {
+                    cnt.boxes += 4;
+                    cnt.wnode += wave_leader();
+                    if (__ballot(node != nu) == 0) cnt.wnode_uniform += wave_leader();
+                }
+                // stk[sp + m] = s_(nhit-1-m): the hits after the nearest, farthest deepest; slots at or above
+                // the new top are scratch (the allocation has three entries of slack above the deepest stack,
+                // scene_build.cpp stack_w4)
+                int16_t* const wstk = stk;
+                wstk[sp * 64] = (int16_t)(nhit == 4u ? s3 : (nhit == 3u ? s2 : s1));
+                wstk[(sp + 1u) * 64] = (int16_t)(nhit == 4u ? s2 : s1);
+                wstk[(sp + 2u) * 64] = (int16_t)s1;
+                uint32_t nxt = nhit != 0u ? (s0 & 0xffffu) : top1;
+                uint32_t nsp = sp + nhit - 1u;
+                const bool postpone = nxt >= 0x8000u && leaf == 0;
+                const uint32_t after_top = nhit >= 2u ? (s1 & 0xffffu) : (nhit == 1u ? top1 : top2);
+                leaf = postpone ? nxt : leaf;
+                nxt = postpone ? after_top : nxt;
+                nsp = postpone ? nsp - 1u : nsp;
+                node = nxt;
+                sp = nsp;
+                if (__ballot(leaf == 0) == 0) break;
+                continue;
+            }
             float c0min, c0max, c1min, c1max;
             uint32_t ch0, ch1;
             // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0) for a
@@ -1387,6 +1462,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_HALF ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes32, (short)0, (int)(P.num_nodes * 32u), 0x00020000)
         : NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+        : NODES == NODES_W4 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes_w4, (short)0, (int)(P.num_nodes_w4 * 104u), 0x00020000)
                             : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rrsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
@@ -1420,7 +1496,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
     while (true) {
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_W4 ? (const float4*)P.nodes_w4 : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -1506,6 +1582,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(con
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_HALF ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes32, (short)0, (int)(P.num_nodes * 32u), 0x00020000)
         : NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+        : NODES == NODES_W4 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes_w4, (short)0, (int)(P.num_nodes_w4 * 104u), 0x00020000)
                             : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rrsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
@@ -1524,7 +1601,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(con
     const uint32_t threshold = P.regen_threshold;
 
     while (true) {
-        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_W4 ? (const float4*)P.nodes_w4 : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
         uint32_t sample, depth, rays;
@@ -1709,6 +1786,7 @@ struct Variant {
     bool half = false;        // binary16 child boxes (32-B nodes)
     int wpg = 1;              // v3/v4: independent waves per workgroup (block = 64 · wpg)
     bool compact = false;     // v3: 13-word parking (needs spp < 8192, max_depth < 64, spp · max_depth < 8192)
+    bool w4 = false;          // v3: 4-wide BVH (NODES_W4)
 };
 
 // rt_set_variant(i) selects kVariants[i]
@@ -1735,6 +1813,10 @@ constexpr Variant kVariants[] = {
     {false, dev::STACK_LDS16, 1, 0, true, 256, false, false, 4, true}, {false, dev::STACK_LDS16, 8, 0, true, 256, false, false, 4, true},
     // 32, 33: 13 (one wave per workgroup) with compact parking, ≤ 64 VGPRs (32) or the compiler's choice (33)
     {false, dev::STACK_LDS16, 8, 0, true, 64, false, false, 1, true}, {false, dev::STACK_LDS16, 1, 0, true, 64, false, false, 1, true},
+    // 34: 13 over the 4-wide BVH; 35, 36: the same held to 6 / 7 waves per SIMD by registers
+    {false, dev::STACK_LDS16, 1, 0, true, 64, false, false, 1, false, true},
+    {false, dev::STACK_LDS16, 6, 0, true, 64, false, false, 1, false, true},
+    {false, dev::STACK_LDS16, 7, 0, true, 64, false, false, 1, false, true},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 
@@ -1805,6 +1887,9 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
     case 31: return v3_pick<8, dev::NODES_48, 4, false, true>(count, tex);
     case 32: return v3_pick<8, dev::NODES_48, 1, false, true>(count, tex);
     case 33: return v3_pick<1, dev::NODES_48, 1, false, true>(count, tex);
+    case 34: return v3_pick<1, dev::NODES_W4>(count, tex);
+    case 35: return v3_pick<6, dev::NODES_W4>(count, tex);
+    case 36: return v3_pick<7, dev::NODES_W4>(count, tex);
     default: return v4_pick<7, dev::NODES_64>(count, tex);
     }
 }
@@ -2029,6 +2114,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.nodes = (const float4*)S.nodes;
     P.nodes48 = (const float4*)S.nodes48;
     P.refs16 = (const uint32_t*)S.refs16;
+    P.nodes_w4 = (const float*)S.nodes_w4;
+    P.num_nodes_w4 = S.num_nodes_w4;
     P.nodes32 = (const uint32_t*)S.nodes32;
     P.prims = (const float4*)S.prims;
     P.mats = (const float4*)S.mats;
@@ -2113,6 +2200,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (kVariants[variant].compact &&
         !(a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u))
         variant = variant == 30 ? 25 : (variant == 31 ? 29 : (variant == 32 ? 15 : 13));  // packed counters would overflow
+    if (kVariants[variant].w4 && (S.num_nodes_w4 == 0 || S.num_nodes_w4 >= (uint32_t)dev::kSentinel16))
+        variant = 13;  // no 4-wide tree (empty scene) or its references do not fit 16 bits
     if (kVariants[variant].persistent && (a->samples_per_pixel == 0 || a->max_depth == 0))
         variant = kVariants[variant].half ? 18 : 13;  // the persistent kernel assumes every pixel traces a ray
     if (philox && !philox_capable(variant)) {
@@ -2131,7 +2220,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // v3/v4: per wave, the parked path state + a 16-bit stack of depth + 3 entries (two sentinel pads)
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
                                   ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
-                                        (size_t)(S.depth + 3) * 64 * 2 +
+                                        (size_t)(V.w4 ? S.stack_w4 + 5 : S.depth + 3) * 64 * 2 +
                                         (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);

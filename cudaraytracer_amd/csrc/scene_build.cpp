@@ -7,6 +7,8 @@
 // SAH build over padded reference boxes produces a BVH with the same closest-hit semantics: the
 // primitive tests alone decide the hit, boxes only cull (see rt_internal.h).
 #include <algorithm>
+#include <functional>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -196,6 +198,80 @@ struct Builder {
     }
 };
 
+// 4-wide BVH from the binary one: each 4-wide node takes a binary node's two children and repeatedly
+// opens the internal child with the largest surface area until it holds four children or only leaves
+// (the usual collapse; the traversal then needs half as many dependent node fetches per ray).  Leaf
+// references are the binary tree's; internal references are 4-wide node indices (pre-order, root 0).
+void collapse_w4(const Builder& B, HostScene* out) {
+    out->nodes_w4.clear();
+    out->num_nodes_w4 = 0;
+    out->depth_w4 = 0;
+    out->stack_w4 = 0;
+    if (B.nodes.empty()) return;
+    struct Slot { Box box; int ref; };
+    std::vector<std::array<Slot, 4>> w4;
+    std::vector<int> count;
+    uint32_t max_depth = 0;
+    std::function<int(int, uint32_t)> make = [&](int bin, uint32_t depth) -> int {
+        std::array<Slot, 4> s;
+        int n = 2;
+        s[0] = {B.nodes[bin].box[0], B.nodes[bin].child[0]};
+        s[1] = {B.nodes[bin].box[1], B.nodes[bin].child[1]};
+        while (n < 4) {
+            int best = -1;
+            float best_area = -1.0f;
+            for (int i = 0; i < n; i++)
+                if (s[i].ref >= 0 && s[i].box.area() > best_area) { best = i; best_area = s[i].box.area(); }
+            if (best < 0) break;
+            const Builder::Node& c = B.nodes[s[best].ref];
+            s[best] = {c.box[0], c.child[0]};
+            s[n++] = {c.box[1], c.child[1]};
+        }
+        const int id = (int)w4.size();
+        w4.push_back(s);
+        count.push_back(n);
+        max_depth = std::max(max_depth, depth);
+        for (int i = 0; i < n; i++)
+            if (w4[id][i].ref >= 0) {
+                const int child = make(w4[id][i].ref, depth + 1);
+                w4[id][i].ref = child;
+            }
+        return id;
+    };
+    make(0, 1);
+    // deepest stack: a visit defers at most (children - 1) entries, so the bound is the largest sum of
+    // (children - 1) along a root-to-leaf path (children precede parents in reverse pre-order)
+    std::vector<uint32_t> defer(w4.size(), 0);
+    for (size_t i = w4.size(); i-- > 0;) {
+        uint32_t below = 0;
+        for (int c = 0; c < count[i]; c++)
+            if (w4[i][c].ref >= 0) below = std::max(below, defer[(size_t)w4[i][c].ref]);
+        defer[i] = (uint32_t)(count[i] - 1) + below;
+    }
+    out->stack_w4 = defer[0];
+    out->num_nodes_w4 = (uint32_t)w4.size();
+    out->depth_w4 = max_depth;
+    out->nodes_w4.assign((size_t)out->num_nodes_w4 * 26, 0.0f);
+    for (size_t i = 0; i < w4.size(); i++) {
+        float* o = out->nodes_w4.data() + i * 26;
+        uint16_t refs[4];
+        for (int c = 0; c < 4; c++) {
+            if (c < count[i]) {
+                const Box& b = w4[i][c].box;
+                o[6 * c + 0] = b.lo[0]; o[6 * c + 1] = b.hi[0];
+                o[6 * c + 2] = b.lo[1]; o[6 * c + 3] = b.hi[1];
+                o[6 * c + 4] = b.lo[2]; o[6 * c + 5] = b.hi[2];
+                refs[c] = (uint16_t)((uint32_t)w4[i][c].ref & 0xffffu);  // valid when refs fit int16
+            } else {  // empty slot: lo > hi on every axis, so the slab test never reports a hit
+                for (int a = 0; a < 3; a++) { o[6 * c + 2 * a] = 3e38f; o[6 * c + 2 * a + 1] = -3e38f; }
+                refs[c] = 0x7fffu;
+            }
+        }
+        o[24] = bits_to_float((uint32_t)refs[0] | ((uint32_t)refs[1] << 16));
+        o[25] = bits_to_float((uint32_t)refs[2] | ((uint32_t)refs[3] << 16));
+    }
+}
+
 int check_texture(const rt_texture_desc& t, uint32_t num_images, std::string* err) {
     if (t.type < RT_CONSTANT || t.type > RT_IMAGE) {
         *err = "texture type " + std::to_string(t.type) + " is not CONSTANT/CHECKER/IMAGE";
@@ -360,6 +436,7 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         o[7] = 0u;
     }
     if (!out->has_half_nodes) out->nodes32.clear();
+    collapse_w4(B, out);
     out->prims.resize((size_t)out->num_prims * 8);
     out->prim_source.resize(out->num_prims);
     for (uint32_t i = 0; i < out->num_prims; i++) {

@@ -23,7 +23,7 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = list(range(34))
+VARIANTS = list(range(37))
 # v3 (13), persistent v4 (16), binary16 nodes (18), persistent + binary16 (19)
 KEY_VARIANTS = [13, 16, 18, 19]
 
