@@ -662,13 +662,13 @@ __device__ __forceinline__ Rng load_rng(const uint32_t* st) {
 // ---------------------------------------------------------------------------------------------------
 struct RngPhilox {
     uint32_t n, r0, r1, r2, r3, pix;
+    uint32_t k0, k1, frame;  // launch-uniform key and frame, read once when the stream is (un)parked
 };
 
 // Block `blk` of the lane's stream: philox10(ctr = {blk, frame, pixel, 0}, key = seed) into s.r0..r3.
 __device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
-    KParamsC* q = kparams_reload();
-    uint32_t c0 = blk, c1 = q->rng_frame, c2 = s.pix, c3 = 0u;
-    uint32_t k0 = q->rng_key_lo, k1 = q->rng_key_hi;
+    uint32_t c0 = blk, c1 = s.frame, c2 = s.pix, c3 = 0u;
+    uint32_t k0 = s.k0, k1 = s.k1;
 #pragma unroll
     for (int i = 0; i < 10; i++) {  // single_round + bumpkey (rocrand_philox4x32_10.h:286-303)
         const uint64_t m0 = (uint64_t)0xD2511F53u * c0;  // one v_mad_u64_u32 for lo and hi
@@ -691,8 +691,12 @@ __device__ __forceinline__ float philox_to_uniform(uint32_t x) {
 }
 
 // Word j (0..3) of the current block.
+// (Two selects on the index bits: LLVM turned the equivalent compare chain into a private array with
+// a lane-varying index, i.e. scratch stores and loads on every draw.)
 __device__ __forceinline__ uint32_t philox_word(const RngPhilox& s, uint32_t j) {
-    return j < 2u ? (j == 0u ? s.r0 : s.r1) : (j == 2u ? s.r2 : s.r3);
+    const bool odd = (j & 1u) != 0u, high = (j & 2u) != 0u;
+    const uint32_t lo = odd ? s.r1 : s.r0, hi = odd ? s.r3 : s.r2;
+    return high ? hi : lo;
 }
 
 __device__ __forceinline__ float uniform(RngPhilox& s) {
@@ -736,7 +740,8 @@ __device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPh
 template <class R> __device__ __forceinline__ R begin_rng(const uint32_t* st, uint32_t pixel);
 template <> __device__ __forceinline__ Rng begin_rng<Rng>(const uint32_t* st, uint32_t) { return load_rng(st); }
 template <> __device__ __forceinline__ RngPhilox begin_rng<RngPhilox>(const uint32_t*, uint32_t pixel) {
-    return RngPhilox{0u, 0u, 0u, 0u, 0u, pixel};
+    KParamsC* q = kparams_reload();
+    return RngPhilox{0u, 0u, 0u, 0u, 0u, pixel, q->rng_key_lo, q->rng_key_hi, q->rng_frame};
 }
 
 // Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop: every
@@ -1085,8 +1090,10 @@ __device__ __forceinline__ void unpark_rng(const uint32_t* park, Rng& r) {
             park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
 }
 __device__ __forceinline__ void unpark_rng(const uint32_t* park, RngPhilox& r) {
+    KParamsC* q = kparams_reload();
     r = RngPhilox{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
-                  park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
+                  park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64],
+                  q->rng_key_lo, q->rng_key_hi, q->rng_frame};
 }
 
 template <bool COMPACT = false, class R>
@@ -2187,12 +2194,12 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
     const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
     int variant = g_variant;
-    // auto: the fastest measured kernel per workload shape (profiles/r01_*): the persistent v4 for short
-    // or deep paths per pixel (config 5: 1 spp, 0.54 vs 0.80 ms; config 3: depth 16, 457 vs 467 ms), v3
-    // with four independent waves per workgroup for the many-sample frames (config 2: 64 spp, 25.7-26.2
-    // vs 26.5-26.9 ms for one wave per workgroup, 27.4-27.8 ms for v4)
+    // auto: the fastest measured kernel per workload shape (profiles/r01c_*): the persistent v4 when a pixel
+    // has few paths (config 5: 1 spp, 0.51-0.54 vs 0.80 ms), v3 with the adaptive longest-first tile order
+    // otherwise (config 2: 17.8 vs 19+ ms; config 3, depth 16: 366 vs 408 ms with XORWOW, within 2 % with
+    // Philox)
     if (variant < 0 || variant >= kNumVariants)
-        variant = (a->samples_per_pixel < 32 || a->max_depth > 8) ? 22 : 13;
+        variant = a->samples_per_pixel < 32 ? 22 : 13;
     if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
         variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
     if (kVariants[variant].half && !S.has_half_nodes)  // a plane beyond the binary16 range: f32 boxes

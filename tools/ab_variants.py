@@ -15,6 +15,7 @@ ap.add_argument("--thresholds", default="40", help="regen thresholds to try for 
 ap.add_argument("--leafmax", default="4", help="BVH leaf sizes to try (RT_TUNE_LEAF_MAX)")
 ap.add_argument("--pwaves", default="0", help="persistent grid waves/SIMD to try (RT_TUNE_PERSISTENT_WAVES)")
 ap.add_argument("--sah", default="12", help="SAH traversal costs x10 to try (RT_TUNE_SAH_TRAVERSAL)")
+ap.add_argument("--rng", default="xorwow", choices=("xorwow", "philox"))
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 if args.spp:
@@ -34,7 +35,7 @@ for lm in sorted({v[2] for v in variants}):
     scenes_by_lm[lm] = DeviceScene(scenes.builtin(cfg.scene))
 lib().rt_set_tuning(1, 4)
 lib().rt_set_tuning(3, 12)
-r = Renderer(cfg.width, cfg.height)
+r = Renderer(cfg.width, cfg.height, rng=args.rng)
 r.render_init()
 inp = cfg.inputs()
 times = {v: [] for v in variants}
@@ -60,4 +61,4 @@ for rnd in range(args.rounds):
         rays[v] = int(r.counters[0])
 for v in variants:
     med = statistics.median(times[v])
-    print(f"{args.config} variant {v[0]} thr {v[1]} leafmax {v[2][0]} sah {v[2][1]} pwaves {v[3]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)
+    print(f"{args.config} {args.rng} variant {v[0]} thr {v[1]} leafmax {v[2][0]} sah {v[2][1]} pwaves {v[3]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)

@@ -7,7 +7,7 @@ from cudaraytracer_amd._lib import lib
 from cudaraytracer_amd.renderer import DeviceScene, Renderer
 cfg = scenes.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
 ds = DeviceScene(scenes.builtin(cfg.scene))
-r = Renderer(cfg.width, cfg.height)
+r = Renderer(cfg.width, cfg.height, rng=os.environ.get("RT_RNG", "xorwow"))
 r.render_init()
 for v in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "6,8").split(",")]:
     lib().rt_set_variant(v)
