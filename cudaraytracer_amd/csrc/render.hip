@@ -415,15 +415,14 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 // emission, or Scatter of the hit material.  Returns true when the path ended (contribution in `contrib`,
 // `emitted * cur_attenuation` or `cur_attenuation * sky`); false when it continues with (ro, rd, att).
 template <bool TEX = true, class PP, class R>
-__device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, int hit, float t, f3& ro,
-                                      f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
+__device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
+                                      f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
     // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
+    // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
+    // primitive — the material load need not wait for the primitive's
     uint32_t mtype = 0xffu;  // 0xff: miss
-    if (hit >= 0) {
-        const uint32_t tag = __float_as_uint(prims[2 * hit + 1].w);
-        mtype = __float_as_uint(P->mats[3 * (tag >> 4)].x) & 15u;
-    }
+    if (hit >= 0) mtype = __float_as_uint(P->mats[3 * (hit_tag >> 4)].x) & 15u;
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
 #ifdef RT_PAD_SHADE
     for (int pad = 0; pad < RT_PAD_SHADE; pad++) asm volatile("v_mov_b32 %0, %0" : "+v"(t));
@@ -436,8 +435,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
     }
     const float4 p0 = prims[2 * hit + 0];
     const float4 p1 = prims[2 * hit + 1];
-    const uint32_t tag = __float_as_uint(p1.w);
-    const uint32_t type = tag & 15u, mat = tag >> 4;
+    const uint32_t type = hit_tag & 15u, mat = hit_tag >> 4;
     const float4 m0 = P->mats[3 * mat + 0];
     const uint32_t ttype = (__float_as_uint(m0.x) >> 4) & 15u;
     f3 p, normal;
@@ -797,7 +795,7 @@ __global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KP
                 float t;
                 const int hit = trace<STACK, COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, lds_stack, cnt);
                 if (COUNT_TESTS) cnt.wshade += wave_leader();
-                done = shade(&P, prims, hit, t, ro, rd, att, rng, rtl, contrib);
+                done = shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib);
                 if (!done) depth++;
             }
             if (done) {
@@ -995,7 +993,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void render_kernel_v2(const 
         if (mode == MODE_SHADE) {
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            if (shade(&P, prims, hit, t_best, ro, rd, att, rng, rtl, contrib)) {
+            if (shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t_best, ro, rd, att, rng, rtl, contrib)) {
                 next_sample(contrib);
             } else if (++depth >= P.max_depth) {
                 next_sample(mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
@@ -1032,6 +1030,7 @@ __host__ __device__ constexpr int park_words(bool compact) { return compact ? PK
 // Traversal cursor of one lane (v3).
 struct Cursor {
     int node, leaf, hit;
+    uint32_t tag;  // type | material << 4 of the closest primitive so far
     uint32_t sp;
     float t_best;
     int mode;
@@ -1170,6 +1169,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     // references (int16 < 0 in the layout) >= 0x8000; leaf == 0: no postponed leaf
     uint32_t node = (uint32_t)c.node, leaf = (uint32_t)c.leaf;
     int hit = c.hit;
+    uint32_t tag = c.tag;
     uint32_t sp = c.sp;
     float t_best = c.t_best;
     const float a_dd = dot(rd, rd);
@@ -1402,11 +1402,13 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                         if (t < t_best && t > kTmin) {
                             t_best = t;
                             hit = (int)i;
+                            tag = __float_as_uint(p1.w);
                         } else {
                             t = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
                             if (t < t_best && t > kTmin) {
                                 t_best = t;
                                 hit = (int)i;
+                            tag = __float_as_uint(p1.w);
                             }
                         }
                     }
@@ -1422,6 +1424,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                         if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
                             t_best = t;
                             hit = (int)i;
+                            tag = __float_as_uint(p1.w);
                         }
                     }
                 }
@@ -1444,6 +1447,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     c.node = (int)node;
     c.leaf = (int)leaf;
     c.hit = hit;
+    c.tag = tag;
     c.sp = sp;
     c.t_best = t_best;
     if (c.node == kSentinel16 && c.leaf == 0) c.mode = MODE_SHADE;
@@ -1485,7 +1489,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
 
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
-    Cursor c{kSentinel16, 0, -1, 0u, FLT_MAX, MODE_DONE};
+    Cursor c{kSentinel16, 0, -1, 0u, 0u, FLT_MAX, MODE_DONE};
 
     {  // first camera ray of the pixel
         uint32_t* st = P.state + pix * 12;
@@ -1514,7 +1518,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
             v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.t_best, ro, rd, att, rng, rtl, contrib);
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib);
             if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
@@ -1601,7 +1605,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(con
 
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
-    Cursor c{kSentinel16, 0, -1, 0u, FLT_MAX, MODE_NEED};
+    Cursor c{kSentinel16, 0, -1, 0u, 0u, FLT_MAX, MODE_NEED};
     uint32_t wq_next = 0u, wq_end = 0u;  // wave-uniform: the wave's current chunk of work indices
     bool drained = false;                // wave-uniform: the frame's queue is empty
     uint32_t wave_pixels = 0u;           // wave-uniform: pixels this wave has taken
@@ -1618,7 +1622,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(con
             v3_unpark(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.t_best, ro, rd, att, rng, rtl, contrib);
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib);
             if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
