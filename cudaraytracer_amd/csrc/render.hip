@@ -1016,7 +1016,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void render_kernel_v2(const 
 //   * 16-bit traversal stack entries in LDS (node and leaf references fit a signed 16 bits when the
 //     scene has < 32767 nodes and < 8192 primitives; rt_render falls back to v2 otherwise);
 //   * the lane's ray count is parked with the path state; primary samples = spp per pixel.
-// LDS per wave: 15 × 256 B of parked state + (depth + 3) × 128 B of stack (2 sentinel pads).
+// LDS per wave: 15 × 256 B of parked state + (depth + 2) × 128 B of stack (2 sentinel pads).
 // ---------------------------------------------------------------------------------------------------
 constexpr int kSentinel16 = 0x7fff;
 constexpr uint32_t kStackBase = 2;  // v3 stack entries start above two sentinel pads
@@ -1563,7 +1563,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
 //   result does not depend on which lane or wave renders it.  Every wave exits once the queue is empty
 //   and its lanes are done (no wave waits on another).
 // Requires spp ≥ 1 and max_depth ≥ 1 (rt_render uses v3 otherwise).
-// LDS per wave: 18 × 256 B of parked state + (depth + 3) × 128 B of stack.
+// LDS per wave: 18 × 256 B of parked state + (depth + 2) × 128 B of stack.
 // ---------------------------------------------------------------------------------------------------
 enum ParkSlotV4 { PK_X = PK_WORDS, PK_G = PK_WORDS + 1, PK_PIX = PK_WORDS + 2, PK_WORDS4 = PK_WORDS + 3 };
 constexpr int MODE_NEED = 3;  // v4: lane waits for a pixel
@@ -1849,7 +1849,10 @@ KernelFn v4_pick(bool count, bool tex) {
 }
 
 // Kernels with the Philox engine (RT_FLAG_RNG_PHILOX): the v3/v4 variants the automatic choice uses.
-constexpr int kPhiloxVariants[] = {13, 22, 25};
+#ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the Philox build of variant 33
+#define RT_PHILOX_COMPACT_W 1
+#endif
+constexpr int kPhiloxVariants[] = {13, 22, 25, 33};
 bool philox_capable(int variant) {
     for (int v : kPhiloxVariants)
         if (v == variant) return true;
@@ -1861,6 +1864,7 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
         switch (variant) {
         case 13: return v3_pick<1, dev::NODES_48, 1, true>(count, tex);
         case 22: return v4_pick<1, dev::NODES_64, 1, true>(count, tex);
+        case 33: return v3_pick<RT_PHILOX_COMPACT_W, dev::NODES_48, 1, true, true>(count, tex);
         default: return v3_pick<1, dev::NODES_48, 4, true>(count, tex);  // 25
         }
     }
@@ -2198,12 +2202,13 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
     const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
     int variant = g_variant;
-    // auto: the fastest measured kernel per workload shape (profiles/r01c_*): the persistent v4 when a pixel
-    // has few paths (config 5: 1 spp, 0.51-0.54 vs 0.80 ms), v3 with the adaptive longest-first tile order
-    // otherwise (config 2: 17.8 vs 19+ ms; config 3, depth 16: 366 vs 408 ms with XORWOW, within 2 % with
-    // Philox)
+    // auto: the fastest measured kernel per workload shape (profiles/r01d_*, r01e_*): the persistent v4 when a
+    // pixel has few paths (config 5: 1 spp, 0.51-0.54 vs 0.80 ms), otherwise v3 with the adaptive
+    // longest-first tile order and compact parking (33): 13 words of parked state + a depth + 2 stack fit
+    // config 2's wave in 5 KB of LDS, 8 waves per SIMD (config 2: 17.05 vs 17.8 ms for 13; config 3, depth
+    // 16: 365 vs 408 ms for v4).  33 falls back to 13 where the packed counters would overflow.
     if (variant < 0 || variant >= kNumVariants)
-        variant = a->samples_per_pixel < 32 ? 22 : 13;
+        variant = a->samples_per_pixel < 32 ? 22 : 33;
     if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
         variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
     if (kVariants[variant].half && !S.has_half_nodes)  // a plane beyond the binary16 range: f32 boxes
@@ -2228,10 +2233,13 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
     }
-    // v3/v4: per wave, the parked path state + a 16-bit stack of depth + 3 entries (two sentinel pads)
+    // v3/v4: per wave, the parked path state + a 16-bit stack of depth + 2 entries: two sentinel pads, and
+    // a visit at level L (root = 1) holds at most L - 1 deferred children, so its unconditional write of
+    // the far child lands at index 2 + (L - 1) <= depth + 1 (the 128-B saving keeps config 2's wave
+    // inside 11 × 512 B of LDS)
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
                                   ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
-                                        (size_t)(V.w4 ? S.stack_w4 + 5 : S.depth + 3) * 64 * 2 +
+                                        (size_t)(V.w4 ? S.stack_w4 + 5 : S.depth + 2) * 64 * 2 +
                                         (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);

@@ -360,7 +360,7 @@ def test_scene_beyond_binary16_range_matches_oracle(variant):
 # ---------------------------------------------------------------------------------------------------
 # Perf-mode RNG (RT_FLAG_RNG_PHILOX): bit-exact with the oracle's Philox restatement, no state buffer
 # ---------------------------------------------------------------------------------------------------
-PHILOX_KERNELS = [-1, 13, 22, 25, 16]  # auto, v3, v4, v3 × 4 waves/WG; 16 (no Philox build) maps to 22
+PHILOX_KERNELS = [-1, 13, 22, 25, 33, 16]  # auto, v3, v4, v3 × 4 waves/WG, v3 compact; 16 (no Philox build) maps to 22
 
 
 @pytest.mark.parametrize("variant", PHILOX_KERNELS)
