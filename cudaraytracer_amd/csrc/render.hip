@@ -1849,6 +1849,9 @@ KernelFn v4_pick(bool count, bool tex) {
 }
 
 // Kernels with the Philox engine (RT_FLAG_RNG_PHILOX): the v3/v4 variants the automatic choice uses.
+#ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the non-texture Philox build of variant 33
+#define RT_PHILOX_COMPACT_W 1
+#endif
 constexpr int kPhiloxVariants[] = {13, 22, 25, 33};
 bool philox_capable(int variant) {
     for (int v : kPhiloxVariants)
@@ -1861,10 +1864,10 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
         switch (variant) {
         case 13: return v3_pick<1, dev::NODES_48, 1, true>(count, tex);
         case 22: return v4_pick<1, dev::NODES_64, 1, true>(count, tex);
-        case 33:  // held to 64 VGPRs (8 waves/SIMD; one 8-B spill of the pixel offset, stored at the start,
-                  // reloaded at the end); the texture build would spill in its loops, so it keeps W = 1
+        case 33:  // W = 8 (64 VGPRs, one cold 8-B spill) lost to W = 1 in a same-box A/B (c2 median 22.5-22.8
+                  // vs 21.6-21.9 ms, profiles/r01f_ab_philox_w1_w8_c2.txt); -DRT_PHILOX_COMPACT_W=8 rebuilds it
             return tex ? v3_pick<1, dev::NODES_48, 1, true, true>(count, true)
-                       : v3_pick<8, dev::NODES_48, 1, true, true>(count, false);
+                       : v3_pick<RT_PHILOX_COMPACT_W, dev::NODES_48, 1, true, true>(count, false);
         default: return v3_pick<1, dev::NODES_48, 4, true>(count, tex);  // 25
         }
     }
