@@ -40,7 +40,6 @@ EXPORTED = [
     "rt_camera_inputs",
     "rt_reference_graph_flatten",
     "rt_build_host_tables",
-    "rt_build_host_half_nodes",
 ]
 
 _lib = None
@@ -80,7 +79,6 @@ def _declare(lib: C.CDLL) -> None:
                                                P(C.c_uint32), P(abi.ImageDesc), P(C.c_uint32)]
     lib.rt_build_host_tables.argtypes = [P(abi.SceneDesc), P(C.c_float), P(C.c_float), P(C.c_float),
                                          P(C.c_int32), P(abi.HostTablesInfo)]
-    lib.rt_build_host_half_nodes.argtypes = [P(abi.SceneDesc), P(C.c_uint32), P(C.c_uint32)]
     lib.LaunchKernel.argtypes = [vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint, vp, vp, abi.InputStruct]
     lib.LaunchKernel.restype = None
     lib.LaunchRandInit.argtypes = [vp]

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <new>
+#include <stdexcept>
 #include <cstring>
 #include <mutex>
 #include <unordered_set>
@@ -16,6 +18,21 @@ namespace rt {
 static thread_local std::string g_last_error;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+// Host steps allocate (std::vector, std::string): a failed allocation must come back as a status code, not
+// as an exception through the extern "C" boundary (which would terminate the caller's process).
+template <class F>
+static int guarded(const char* what, F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        set_error(std::string(what) + ": host allocation failed");
+        return RT_ERR_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        set_error(std::string(what) + ": " + e.what());
+        return RT_ERR_INVALID_SCENE;
+    }
+}
 
 static int hip_fail(hipError_t e, const char* what) {
     set_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -37,9 +54,7 @@ static void free_device(DeviceScene* s) {
     if (s->nodes) (void)hipFree((void*)s->nodes);
     if (s->nodes48) (void)hipFree((void*)s->nodes48);
     if (s->refs16) (void)hipFree((void*)s->refs16);
-    if (s->nodes32) (void)hipFree((void*)s->nodes32);
-    if (s->nodes_w4) (void)hipFree((void*)s->nodes_w4);
-    s->nodes48 = s->refs16 = s->nodes32 = s->nodes_w4 = nullptr;
+    s->nodes48 = s->refs16 = nullptr;
     if (s->prims) (void)hipFree((void*)s->prims);
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);
@@ -61,13 +76,6 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     d.nodes48 = p;
     if ((rc = upload(h.refs16, &p, "hipMalloc/hipMemcpy(refs16)"))) goto fail;
     d.refs16 = p;
-    if ((rc = upload(h.nodes32, &p, "hipMalloc/hipMemcpy(nodes32)"))) goto fail;
-    d.nodes32 = p;
-    if ((rc = upload(h.nodes_w4, &p, "hipMalloc/hipMemcpy(nodes_w4)"))) goto fail;
-    d.nodes_w4 = p;
-    d.num_nodes_w4 = h.num_nodes_w4;
-    d.depth_w4 = h.depth_w4;
-    d.stack_w4 = h.stack_w4;
     if ((rc = upload(h.prims, &p, "hipMalloc/hipMemcpy(prims)"))) goto fail;
     d.prims = p;
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
@@ -82,7 +90,6 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;
-    d.has_half_nodes = h.has_half_nodes;
     d.device_bytes = (h.nodes.size() + h.prims.size() + h.mats.size()) * 4 + h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;
@@ -227,22 +234,26 @@ int rt_set_device(int device) {
 int rt_scene_create(const rt_scene_desc* desc, rt_scene** out_scene) {
     if (!out_scene) { set_error("rt_scene_create: out_scene is NULL"); return RT_ERR_INVALID_ARGUMENT; }
     *out_scene = nullptr;
-    HostScene h;
-    std::string err;
-    int rc = build_host_scene(desc, &h, &err);
-    if (rc) { set_error("rt_scene_create: " + err); return rc; }
-    return create_device_scene(h, out_scene);
+    return guarded("rt_scene_create", [&]() -> int {
+        HostScene h;
+        std::string err;
+        int rc = build_host_scene(desc, &h, &err);
+        if (rc) { set_error("rt_scene_create: " + err); return rc; }
+        return create_device_scene(h, out_scene);
+    });
 }
 
 int rt_scene_from_reference_graph(const void* world, rt_scene** out_scene) {
     if (!out_scene) { set_error("rt_scene_from_reference_graph: out_scene is NULL"); return RT_ERR_INVALID_ARGUMENT; }
     *out_scene = nullptr;
-    FlatDesc f;
-    std::string err;
-    int rc = flatten_reference_graph(world, &f, &err);
-    if (rc) { set_error("rt_scene_from_reference_graph: " + err); return rc; }
-    rt_scene_desc d = f.desc();
-    return rt_scene_create(&d, out_scene);
+    return guarded("rt_scene_from_reference_graph", [&]() -> int {
+        FlatDesc f;
+        std::string err;
+        int rc = flatten_reference_graph(world, &f, &err);
+        if (rc) { set_error("rt_scene_from_reference_graph: " + err); return rc; }
+        rt_scene_desc d = f.desc();
+        return rt_scene_create(&d, out_scene);
+    });
 }
 
 int rt_scene_update_materials(rt_scene* scene, const rt_material_desc* materials, uint32_t num_materials) {
@@ -254,22 +265,30 @@ int rt_scene_update_materials(rt_scene* scene, const rt_material_desc* materials
         set_error("rt_scene_update_materials: material count differs from the scene's");
         return RT_ERR_INVALID_ARGUMENT;
     }
-    std::vector<float> packed;
-    std::string err;
-    int rc = pack_materials(materials, num_materials, (uint32_t)(scene->host.imgs.size() / 4), &packed, &err);
-    if (rc) { set_error("rt_scene_update_materials: " + err); return rc; }
-    for (uint32_t i = 0; i < num_materials; i++)
-        if (materials[i].type != RT_DIELECTRIC && materials[i].albedo.type == RT_IMAGE) scene->dev.has_image_textures = true;
-    bool tex = false;
-    for (uint32_t i = 0; i < num_materials; i++)
-        if (materials[i].type != RT_DIELECTRIC && materials[i].albedo.type != RT_CONSTANT) tex = true;
-    scene->dev.has_textures = tex;
-    if (!packed.empty()) {
-        hipError_t e = hipMemcpy((void*)scene->dev.mats, packed.data(), packed.size() * 4, hipMemcpyHostToDevice);
-        if (e != hipSuccess) return hip_fail(e, "rt_scene_update_materials: hipMemcpy");
-    }
-    scene->host.mats = packed;
-    return RT_OK;
+    return guarded("rt_scene_update_materials", [&]() -> int {
+        std::vector<float> packed;
+        std::string err;
+        int rc = pack_materials(materials, num_materials, (uint32_t)(scene->host.imgs.size() / 4), &packed, &err);
+        if (rc) { set_error("rt_scene_update_materials: " + err); return rc; }
+        bool img = false, tex = false;
+        for (uint32_t i = 0; i < num_materials; i++) {
+            if (materials[i].type == RT_DIELECTRIC) continue;
+            img |= materials[i].albedo.type == RT_IMAGE;
+            tex |= materials[i].albedo.type != RT_CONSTANT;
+        }
+        if (!packed.empty()) {
+            // renders are asynchronous on the callers' streams: let every launch that may still read the
+            // old table finish before it is overwritten (the viewer edits between frames, CudaLayer.cpp:719-872)
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) return hip_fail(e, "rt_scene_update_materials: hipDeviceSynchronize");
+            e = hipMemcpy((void*)scene->dev.mats, packed.data(), packed.size() * 4, hipMemcpyHostToDevice);
+            if (e != hipSuccess) return hip_fail(e, "rt_scene_update_materials: hipMemcpy");
+        }
+        scene->dev.has_image_textures = img;
+        scene->dev.has_textures = tex;
+        scene->host.mats = packed;
+        return RT_OK;
+    });
 }
 
 int rt_reference_graph_flatten(const void* world, rt_hittable_desc* hittables, uint32_t* num_hittables,
@@ -280,9 +299,13 @@ int rt_reference_graph_flatten(const void* world, rt_hittable_desc* hittables, u
         return RT_ERR_INVALID_ARGUMENT;
     }
     FlatDesc f;
-    std::string err;
-    int rc = flatten_reference_graph(world, &f, &err);
-    if (rc) { set_error("rt_reference_graph_flatten: " + err); return rc; }
+    int rc = guarded("rt_reference_graph_flatten", [&]() -> int {
+        std::string err;
+        int r = flatten_reference_graph(world, &f, &err);
+        if (r) set_error("rt_reference_graph_flatten: " + err);
+        return r;
+    });
+    if (rc) return rc;
     bool fits = (!hittables || f.hittables.size() <= *num_hittables) &&
                 (!materials || f.materials.size() <= *num_materials) && (!images || f.images.size() <= *num_images);
     if (fits) {
@@ -301,9 +324,13 @@ int rt_build_host_tables(const rt_scene_desc* desc, float* nodes, float* prims, 
                          int32_t* prim_source, rt_host_tables_info* info) {
     if (!info) { set_error("rt_build_host_tables: info is NULL"); return RT_ERR_INVALID_ARGUMENT; }
     HostScene h;
-    std::string err;
-    int rc = build_host_scene(desc, &h, &err);
-    if (rc) { set_error("rt_build_host_tables: " + err); return rc; }
+    int rc = guarded("rt_build_host_tables", [&]() -> int {
+        std::string err;
+        int r = build_host_scene(desc, &h, &err);
+        if (r) set_error("rt_build_host_tables: " + err);
+        return r;
+    });
+    if (rc) return rc;
     info->num_nodes = h.num_nodes;
     info->num_prims = h.num_prims;
     info->num_materials = h.num_mats;
@@ -312,21 +339,6 @@ int rt_build_host_tables(const rt_scene_desc* desc, float* nodes, float* prims, 
     if (prims) std::copy(h.prims.begin(), h.prims.end(), prims);
     if (materials) std::copy(h.mats.begin(), h.mats.end(), materials);
     if (prim_source) std::copy(h.prim_source.begin(), h.prim_source.end(), prim_source);
-    return RT_OK;
-}
-
-int rt_build_host_half_nodes(const rt_scene_desc* desc, uint32_t* nodes32, uint32_t* num_nodes) {
-    if (!num_nodes) { set_error("rt_build_host_half_nodes: num_nodes is NULL"); return RT_ERR_INVALID_ARGUMENT; }
-    HostScene h;
-    std::string err;
-    int rc = build_host_scene(desc, &h, &err);
-    if (rc) { set_error("rt_build_host_half_nodes: " + err); return rc; }
-    *num_nodes = h.num_nodes;
-    if (!h.has_half_nodes) {
-        set_error("rt_build_host_half_nodes: a box plane lies beyond the binary16 range");
-        return RT_ERR_UNSUPPORTED;
-    }
-    if (nodes32) std::copy(h.nodes32.begin(), h.nodes32.end(), nodes32);
     return RT_OK;
 }
 

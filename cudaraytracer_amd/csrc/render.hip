@@ -27,6 +27,7 @@
 #include <cstring>
 #include <atomic>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <type_traits>
 
@@ -42,11 +43,10 @@ namespace dev {
 struct f3 {
     float x, y, z;
 };
-typedef __fp16 half2v __attribute__((ext_vector_type(2)));
-typedef float fl2 __attribute__((ext_vector_type(2)));
 
-// BVH node layouts read by the v3/v4 traversal (template argument NODES)
-enum NodeLayout { NODES_48 = 0, NODES_HALF = 1, NODES_64 = 2, NODES_W4 = 3 };
+// BVH node layouts read by the v3/v4 traversal (template argument NODES): 48 B of child boxes + a
+// separate table of packed 16-bit child references, or the 64-B node with both (rt_internal.h)
+enum NodeLayout { NODES_48 = 0, NODES_64 = 2 };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -143,9 +143,6 @@ struct KParams {
     const float4* nodes;
     const float4* nodes48;   // v3: three box float4 per node
     const uint32_t* refs16;  // v3: packed 16-bit child references
-    const float* nodes_w4;   // v3 NODES_W4: 26 words per 4-wide node (scene_build.cpp collapse_w4)
-    uint32_t num_nodes_w4;
-    const uint32_t* nodes32; // v3/v4 HALF: 32-B nodes with binary16 child boxes
     const float4* prims;
     const float4* mats;
     const int4* imgs;
@@ -182,9 +179,11 @@ struct KParams {
 constexpr int kStackMax = 64;
 constexpr int kBlock = 256;
 
-enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_HYBRID = 2, STACK_LDS16 = 3 };
+// Traversal stack of each kernel family: per-lane scratch array (v1, any scene), 32-bit LDS entries
+// (v2, 32-bit references), 16-bit LDS entries (v3/v4, scenes whose references fit 16 bits)
+enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_LDS16 = 3 };
 
-// Per-lane traversal stacks -------------------------------------------------------------------------
+// Per-lane traversal stack of the v1 kernel (the fallback for scenes the LDS kernels cannot hold)
 struct ScratchStack {
     int s[kStackMax];
     int n;
@@ -193,40 +192,6 @@ struct ScratchStack {
     __device__ __forceinline__ int pop() { return s[--n]; }
     __device__ __forceinline__ bool empty() const { return n == 0; }
 };
-
-struct LdsStack {  // [depth][256] layout: lane-consecutive, bank-conflict free
-    uint32_t* base;
-    int n;
-    __device__ __forceinline__ void init(uint32_t* lds) { base = lds + threadIdx.x; n = 0; }
-    __device__ __forceinline__ void push(int v) { base[(n++) * kBlock] = (uint32_t)v; }
-    __device__ __forceinline__ int pop() { return (int)base[(--n) * kBlock]; }
-    __device__ __forceinline__ bool empty() const { return n == 0; }
-};
-
-struct HybridStack {  // top 4 entries in VGPRs, deeper entries in scratch
-    int r0, r1, r2, r3;
-    int spill[kStackMax];
-    int n;
-    __device__ __forceinline__ void init(uint32_t*) { n = 0; }
-    __device__ __forceinline__ void push(int v) {
-        if (n >= 4) spill[n - 4] = r3;
-        r3 = r2; r2 = r1; r1 = r0; r0 = v;
-        n++;
-    }
-    __device__ __forceinline__ int pop() {
-        int v = r0;
-        r0 = r1; r1 = r2; r2 = r3;
-        n--;
-        if (n >= 4) r3 = spill[n - 4];
-        return v;
-    }
-    __device__ __forceinline__ bool empty() const { return n == 0; }
-};
-
-template <int K> struct StackOf;
-template <> struct StackOf<STACK_SCRATCH> { using T = ScratchStack; };
-template <> struct StackOf<STACK_LDS> { using T = LdsStack; };
-template <> struct StackOf<STACK_HYBRID> { using T = HybridStack; };
 
 struct Counts {
     uint32_t rays, boxes, prims, primary;
@@ -245,10 +210,9 @@ constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX
 
 // Closest hit (BVHNode::Hit, Hittable.cuh:387-439, and the primitive tests of PerformHit :470-485).
 // Returns the primitive index (BVH order) or -1, and the hit distance in t_best.
-template <int STACK, bool COUNT>
+template <bool COUNT>
 __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const float4* __restrict__ prims,
-                                     uint32_t num_nodes, f3 o, f3 d, float a_dd, float& t_best,
-                                     uint32_t* lds_stack, Counts& cnt) {
+                                     uint32_t num_nodes, f3 o, f3 d, float a_dd, float& t_best, Counts& cnt) {
     t_best = FLT_MAX;
     int hit = -1;
     if (num_nodes == 0) return -1;
@@ -260,8 +224,8 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
     const f3 invd = mk(fminf(fmaxf(1.0f / d.x, -1e20f), 1e20f), fminf(fmaxf(1.0f / d.y, -1e20f), 1e20f),
                        fminf(fmaxf(1.0f / d.z, -1e20f), 1e20f));
     const float oix = o.x * invd.x, oiy = o.y * invd.y, oiz = o.z * invd.z;
-    typename StackOf<STACK>::T stack;
-    stack.init(lds_stack);
+    ScratchStack stack;
+    stack.init(nullptr);
     int node = 0;
     while (true) {
         while (node >= 0) {
@@ -360,6 +324,7 @@ __device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, 
     }
     if (tex_type == RT_IMAGE) {
         const int img = __float_as_int(m0.w);
+        if (img < 0) return mk(0.0f, 1.0f, 1.0f);  // no image (Texture.cuh:83-84: data == nullptr → cyan)
         const int4 im = imgs[img];
         if (im.x < 0) return mk(0.0f, 1.0f, 1.0f);  // data == nullptr
         u = clampf(u, 0.0f, 1.0f);
@@ -424,9 +389,6 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
     uint32_t mtype = 0xffu;  // 0xff: miss
     if (hit >= 0) mtype = __float_as_uint(P->mats[3 * (hit_tag >> 4)].x) & 15u;
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
-#ifdef RT_PAD_SHADE
-    for (int pad = 0; pad < RT_PAD_SHADE; pad++) asm volatile("v_mov_b32 %0, %0" : "+v"(t));
-#endif
     if (hit < 0) {  // sky (Kernel.cu:41-44)
         const float tt = 0.5f * (rd.y / length(rd) + 1.0f);
         const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
@@ -742,25 +704,13 @@ template <> __device__ __forceinline__ RngPhilox begin_rng<RngPhilox>(const uint
     return RngPhilox{0u, 0u, 0u, 0u, 0u, pixel, q->rng_key_lo, q->rng_key_hi, q->rng_frame};
 }
 
-// Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop: every
-// iteration traces one ray per lane to completion (trace()), then shades it.
-template <bool SCENE_LDS, int STACK, bool COUNT_TESTS, int WAVES_PER_SIMD>
-__global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KParams P) {
-    extern __shared__ float4 lds[];
+// v1: Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop: every
+// iteration traces one ray per lane to completion (trace(), scratch stack, 32-bit references), then
+// shades it.  The fallback for scenes whose BVH is too large or deep for the LDS-stack kernels.
+template <bool COUNT_TESTS>
+__global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
     const float4* nodes = P.nodes;
     const float4* prims = P.prims;
-    uint32_t* lds_stack = nullptr;
-    if constexpr (SCENE_LDS) {
-        const uint32_t nn = P.num_nodes * 4, np = P.num_prims * 2;
-        for (uint32_t i = threadIdx.x; i < nn; i += kBlock) lds[i] = P.nodes[i];
-        for (uint32_t i = threadIdx.x; i < np; i += kBlock) lds[nn + i] = P.prims[i];
-        __syncthreads();
-        nodes = lds;
-        prims = lds + nn;
-        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)(lds + nn + np);
-    } else {
-        if constexpr (STACK == STACK_LDS) lds_stack = (uint32_t*)lds;
-    }
     uint32_t x, g;
     size_t pix;
     if (!lane_pixel(P, x, g, pix)) return;
@@ -793,7 +743,7 @@ __global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KP
                 cnt.rays++;
                 const float a_dd = dot(rd, rd);
                 float t;
-                const int hit = trace<STACK, COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, lds_stack, cnt);
+                const int hit = trace<COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, cnt);
                 if (COUNT_TESTS) cnt.wshade += wave_leader();
                 done = shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib);
                 if (!done) depth++;
@@ -822,8 +772,8 @@ __global__ __launch_bounds__(kBlock, WAVES_PER_SIMD) void render_kernel(const KP
 constexpr int kSentinel = 0x7fffffff;  // traversal finished (internal node ids are < it, leaves < 0)
 enum LaneMode { MODE_TRAV = 0, MODE_SHADE = 1, MODE_DONE = 2 };
 
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, int BLOCK>
-__global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void render_kernel_v2(const KParams P) {
+template <bool COUNT_TESTS, int BLOCK = 64>
+__global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
     extern __shared__ float4 lds[];
     uint32_t* const stk = (uint32_t*)lds + threadIdx.x;  // [depth][BLOCK] per-lane stacks
     const float4* __restrict__ nodes = P.nodes;
@@ -1187,79 +1137,6 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         while (node < (uint32_t)kSentinel16) {
             const uint32_t top1 = ustk[(sp - 1u) * 64];
             const uint32_t top2 = ustk[(sp - 2u) * 64];
-            if constexpr (NODES == NODES_W4) {
-                // 4-wide node: one key per child, (bits of its entry distance, upper 16) | reference for a hit
-                // and +inf | reference for a miss (entry distances are >= kTmin > 0, so the bits order like
-                // the floats); a 5-exchange network sorts them, the nearest hit is visited next and the other
-                // hits go onto the stack farthest first.  Truncating the distance only reorders near-ties.
-                uint32_t k0, k1, k2, k3;
-                const auto keys = [&](const float4 a, const float4 b, const float4 cq, const float4 d, const float4 e,
-                                      const float4 f, const uint32_t r01, const uint32_t r23) {
-                    const auto key = [&](float lx, float hx, float ly, float hy, float lz, float hz, uint32_t ref) {
-                        const float nx = __builtin_fmaf(lx, pa.x, __builtin_fmaf(hx, pc.x, -oi.x));
-                        const float fx = __builtin_fmaf(hx, pa.x, __builtin_fmaf(lx, pc.x, -oi.x));
-                        const float ny = __builtin_fmaf(ly, pa.y, __builtin_fmaf(hy, pc.y, -oi.y));
-                        const float fy = __builtin_fmaf(hy, pa.y, __builtin_fmaf(ly, pc.y, -oi.y));
-                        const float nz = __builtin_fmaf(lz, pa.z, __builtin_fmaf(hz, pc.z, -oi.z));
-                        const float fz = __builtin_fmaf(hz, pa.z, __builtin_fmaf(lz, pc.z, -oi.z));
-                        const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, kTmin));
-                        const float tf = fminf(fminf(fx, fy), fminf(fz, t_best));
-                        return tn <= tf ? ((__float_as_uint(tn) & 0xffff0000u) | ref) : (0x7f800000u | ref);
-                    };
-                    k0 = key(a.x, a.y, a.z, a.w, b.x, b.y, r01 & 0xffffu);
-                    k1 = key(b.z, b.w, cq.x, cq.y, cq.z, cq.w, r01 >> 16);
-                    k2 = key(d.x, d.y, d.z, d.w, e.x, e.y, r23 & 0xffffu);
-                    k3 = key(e.z, e.w, f.x, f.y, f.z, f.w, r23 >> 16);
-                };
-                const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
-                if (kScalarNodes && __ballot(node != nu) == 0) {
-                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes48 + nu * 104u);
-                    const ConstU32* cr = (const ConstU32*)((const ConstU8*)nodes48 + nu * 104u + 96u);
-                    keys(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
-                         make_float4(cn[8], cn[9], cn[10], cn[11]), make_float4(cn[12], cn[13], cn[14], cn[15]),
-                         make_float4(cn[16], cn[17], cn[18], cn[19]), make_float4(cn[20], cn[21], cn[22], cn[23]),
-                         cr[0], cr[1]);
-                } else {
-                    uint32_t noff;  // node · 104 with the full-rate 24-bit multiply
-                    asm("v_mul_u32_u24 %0, 0x68, %1" : "=v"(noff) : "v"(node));
-                    const uint2 rr = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 96u, 0, 0));
-                    keys(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 48u, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 64u, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 80u, 0, 0)),
-                         rr.x, rr.y);
-                }
-                const uint32_t a0 = min(k0, k1), a1 = max(k0, k1), b0 = min(k2, k3), b1 = max(k2, k3);
-                const uint32_t s0 = min(a0, b0), m1 = max(a0, b0), m2 = min(a1, b1), s3 = max(a1, b1);
-                const uint32_t s1 = min(m1, m2), s2 = max(m1, m2);
-                const uint32_t nhit = (s0 < 0x7f800000u ? 1u : 0u) + (s1 < 0x7f800000u ? 1u : 0u) +
-                                     (s2 < 0x7f800000u ? 1u : 0u) + (s3 < 0x7f800000u ? 1u : 0u);
-                if (COUNT_TESTS) {
-                    cnt.boxes += 4;
-                    cnt.wnode += wave_leader();
-                    if (__ballot(node != nu) == 0) cnt.wnode_uniform += wave_leader();
-                }
-                // stk[sp + m] = s_(nhit-1-m): the hits after the nearest, farthest deepest; slots at or above
-                // the new top are scratch (the allocation has three entries of slack above the deepest stack,
-                // scene_build.cpp stack_w4)
-                int16_t* const wstk = stk;
-                wstk[sp * 64] = (int16_t)(nhit == 4u ? s3 : (nhit == 3u ? s2 : s1));
-                wstk[(sp + 1u) * 64] = (int16_t)(nhit == 4u ? s2 : s1);
-                wstk[(sp + 2u) * 64] = (int16_t)s1;
-                uint32_t nxt = nhit != 0u ? (s0 & 0xffffu) : top1;
-                uint32_t nsp = sp + nhit - 1u;
-                const bool postpone = nxt >= 0x8000u && leaf == 0;
-                const uint32_t after_top = nhit >= 2u ? (s1 & 0xffffu) : (nhit == 1u ? top1 : top2);
-                leaf = postpone ? nxt : leaf;
-                nxt = postpone ? after_top : nxt;
-                nsp = postpone ? nsp - 1u : nsp;
-                node = nxt;
-                sp = nsp;
-                if (__ballot(leaf == 0) == 0) break;
-                continue;
-            }
             float c0min, c0max, c1min, c1max;
             uint32_t ch0, ch1;
             // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0) for a
@@ -1285,29 +1162,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 c1min = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, kTmin));
                 c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best));
             };
-            if constexpr (NODES == NODES_HALF) {  // 32-B node: binary16 planes (exact in f32: v_fma_mix_f32) + refs
-                const uint32_t noff = (uint32_t)node << 5;
-                const uint4 q0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0));
-                const uint4 q1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0));
-                const half2v h0 = __builtin_bit_cast(half2v, q0.x), h1 = __builtin_bit_cast(half2v, q0.y);
-                const half2v h2 = __builtin_bit_cast(half2v, q0.z), h3 = __builtin_bit_cast(half2v, q0.w);
-                const half2v h4 = __builtin_bit_cast(half2v, q1.x), h5 = __builtin_bit_cast(half2v, q1.y);
-                const float4 n0 = make_float4((float)h0.x, (float)h0.y, (float)h1.x, (float)h1.y);
-                const float4 n1 = make_float4((float)h2.x, (float)h2.y, (float)h3.x, (float)h3.y);
-                const float4 n2 = make_float4((float)h4.x, (float)h4.y, (float)h5.x, (float)h5.y);
-                ch0 = q1.z & 0xffffu;
-                ch1 = q1.z >> 16;
-                const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
-                const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
-                const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
-                const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
-                const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
-                const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
-                c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
-                c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
-                c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
-                c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
-            } else if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
+            if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
                 const uint32_t noff = (uint32_t)node << 6;
                 const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
                 ch0 = r2.x & 0xffffu;
@@ -1337,9 +1192,6 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                          __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
                 }
             }
-#ifdef RT_PAD_NODE  // sensitivity experiment: RT_PAD_NODE extra 2-cycle VALU ops per node visit
-            for (int pad = 0; pad < RT_PAD_NODE; pad++) asm volatile("v_mov_b32 %0, %0" : "+v"(c0min));
-#endif
             if (COUNT_TESTS) {
                 cnt.boxes += 2;
                 cnt.wnode += wave_leader();
@@ -1382,10 +1234,6 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 const float4 p0 = prims[2 * i + 0];
                 const float4 p1 = prims[2 * i + 1];
                 const uint32_t type = __float_as_uint(p1.w) & 15u;
-#ifdef RT_PAD_LEAF
-                float padv = p0.x;
-                for (int pad = 0; pad < RT_PAD_LEAF; pad++) asm volatile("v_mov_b32 %0, %0" : "+v"(padv));
-#endif
                 if (COUNT_TESTS) {
                     cnt.prims++;
                     cnt.wleaf += wave_leader();
@@ -1453,34 +1301,28 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     if (c.node == kSentinel16 && c.leaf == 0) c.mode = MODE_SHADE;
 }
 
-// LDS slice of this wave: WPG independent waves share a workgroup (no barriers), each with its own
-// P.lds_wave_words words of parked state + stack.
-__device__ __forceinline__ uint32_t* wave_lds(float4* lds, const KParams& P) {
-    return (uint32_t*)lds + (threadIdx.x >> 6) * P.lds_wave_words;
-}
-
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48, int WPG = 1, bool PHILOX = false,
-          bool COMPACT = false>
-__global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
+// v3 kernel: one wave per workgroup, one 8×8 pixel tile per wave; LDS holds the wave's parked path state
+// and its traversal stacks (P.lds_wave_words words).
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false, bool COMPACT = false>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    constexpr int NODES = NODES_48;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t* const wl = wave_lds(lds, P);
+    uint32_t* const wl = (uint32_t*)lds;
     uint32_t* const park = wl + lane;                                                  // word k: park[k * 64]
     int16_t* const stk = reinterpret_cast<int16_t*>(wl + park_words(COMPACT) * 64) + lane;  // stk[j * 64]
     // node boxes and packed child references through buffer descriptors: 32-bit offsets, no 64-bit
     // address arithmetic per visit; 48 B of boxes + 4 B of references per node
     const __amdgpu_buffer_rsrc_t nrsrc =
-        NODES == NODES_HALF ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes32, (short)0, (int)(P.num_nodes * 32u), 0x00020000)
-        : NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
-        : NODES == NODES_W4 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes_w4, (short)0, (int)(P.num_nodes_w4 * 104u), 0x00020000)
-                            : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+        NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+                          : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rrsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
     const float4* __restrict__ prims = P.prims;
     uint32_t x, g;
     size_t pix;
-    const uint32_t slot = blockIdx.x * WPG + (threadIdx.x >> 6);
+    const uint32_t slot = blockIdx.x;
     const uint32_t tile = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
     if (!lane_pixel<64>(P, x, g, pix, tile)) return;
     const bool rtl = P.rius_rtl != 0;
@@ -1507,7 +1349,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v3(con
     while (true) {
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_W4 ? (const float4*)P.nodes_w4 : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -1582,19 +1424,17 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
     return true;
 }
 
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, int NODES = NODES_48, int WPG = 1, bool PHILOX = false>
-__global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
+template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false>
+__global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t* const wl = wave_lds(lds, P);
+    uint32_t* const wl = (uint32_t*)lds;
     uint32_t* const park = wl + lane;
     int16_t* const stk = reinterpret_cast<int16_t*>(wl + PK_WORDS4 * 64) + lane;
     const __amdgpu_buffer_rsrc_t nrsrc =
-        NODES == NODES_HALF ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes32, (short)0, (int)(P.num_nodes * 32u), 0x00020000)
-        : NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
-        : NODES == NODES_W4 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes_w4, (short)0, (int)(P.num_nodes_w4 * 104u), 0x00020000)
-                            : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+        NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+                          : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rrsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
     const float4* __restrict__ prims = P.prims;
@@ -1612,7 +1452,7 @@ __global__ __launch_bounds__(64 * WPG, WAVES_PER_SIMD) void render_kernel_v4(con
     const uint32_t threshold = P.regen_threshold;
 
     while (true) {
-        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_W4 ? (const float4*)P.nodes_w4 : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
         uint32_t sample, depth, rays;
@@ -1786,129 +1626,56 @@ int hip_check(hipError_t e, const char* what, int code = RT_ERR_DEVICE) {
 
 using KernelFn = void (*)(const dev::KParams);
 
+// The kernels librt_hip.so ships (rt_set_variant(i) selects kVariants[i]).  Round 1 measured 37 variants;
+// the ones that lost their A/B (LDS-staged scene tables, binary16 and 4-wide nodes, several waves per
+// workgroup, register-bound occupancy targets) were dropped (DESIGN.md §4 keeps their numbers).
+//   0  v1: scratch stack, 32-bit references       — fallback for scenes beyond 16-bit references and deep BVHs
+//   1  v2: 64-thread resumable, 32-bit LDS stacks — fallback for scenes beyond 16-bit references
+//   2  v3: 15-word parking                        — spp/depth too large for compact parking
+//   3  v3: 13-word compact parking                — default for spp >= 32
+//   4  v4: persistent work queue, 64-B nodes      — default for spp < 32
 struct Variant {
-    bool scene_lds;
-    int stack;
-    int waves;      // __launch_bounds__ minimum waves per SIMD (1 = compiler's choice)
-    int lds_depth;  // LDS stack entries per lane
-    bool resumable; // render_kernel_v2
-    int block;      // threads per workgroup
-    bool persistent = false;  // render_kernel_v4: device-filling grid + work queue
-    bool half = false;        // binary16 child boxes (32-B nodes)
-    int wpg = 1;              // v3/v4: independent waves per workgroup (block = 64 · wpg)
-    bool compact = false;     // v3: 13-word parking (needs spp < 8192, max_depth < 64, spp · max_depth < 8192)
-    bool w4 = false;          // v3: 4-wide BVH (NODES_W4)
+    int stack;        // StackKind
+    int lds_depth;    // v2: LDS stack entries per lane
+    int block;        // threads per workgroup
+    int kernel;       // 1, 2, 3, 4: v1..v4
+    bool compact;     // v3: 13-word parking (needs spp < 8192, max_depth < 64, spp · max_depth < 8192)
 };
-
-// rt_set_variant(i) selects kVariants[i]
 constexpr Variant kVariants[] = {
-    {false, dev::STACK_SCRATCH, 1, 0, false, 256}, {false, dev::STACK_LDS, 1, 24, false, 256},
-    {false, dev::STACK_HYBRID, 1, 0, false, 256},  {true, dev::STACK_SCRATCH, 1, 0, false, 256},
-    {true, dev::STACK_LDS, 1, 24, false, 256},     {true, dev::STACK_HYBRID, 1, 0, false, 256},
-    {false, dev::STACK_LDS, 6, 20, false, 256},    {false, dev::STACK_LDS, 8, 16, false, 256},
-    {false, dev::STACK_LDS, 1, 24, true, 256},     {false, dev::STACK_LDS, 6, 20, true, 256},
-    {false, dev::STACK_LDS, 8, 16, true, 256},     {false, dev::STACK_LDS, 1, 24, true, 64},
-    {false, dev::STACK_LDS, 6, 24, true, 64},     {false, dev::STACK_LDS16, 1, 0, true, 64},
-    {false, dev::STACK_LDS16, 6, 0, true, 64},     {false, dev::STACK_LDS16, 8, 0, true, 64},
-    {false, dev::STACK_LDS16, 1, 0, true, 64, true}, {false, dev::STACK_LDS16, 6, 0, true, 64, true},
-    {false, dev::STACK_LDS16, 1, 0, true, 64, false, true}, {false, dev::STACK_LDS16, 1, 0, true, 64, true, true},
-    {false, dev::STACK_LDS16, 6, 0, true, 64, true, true},
-    {false, dev::STACK_LDS16, 1, 0, true, 64}, {false, dev::STACK_LDS16, 1, 0, true, 64, true},
-    {false, dev::STACK_LDS16, 7, 0, true, 64, true},
-    // 24..27: v3 / v4 (64-B nodes) with 2 or 4 independent waves per workgroup
-    {false, dev::STACK_LDS16, 1, 0, true, 128, false, false, 2}, {false, dev::STACK_LDS16, 1, 0, true, 256, false, false, 4},
-    {false, dev::STACK_LDS16, 1, 0, true, 128, true, false, 2},  {false, dev::STACK_LDS16, 1, 0, true, 256, true, false, 4},
-    // 28: v3 × 4 waves/WG with binary16 nodes; 29: v3 × 4 waves/WG, ≤ 64 VGPRs (8 waves/SIMD by registers)
-    {false, dev::STACK_LDS16, 1, 0, true, 256, false, true, 4}, {false, dev::STACK_LDS16, 8, 0, true, 256, false, false, 4},
-    // 30, 31: 25 and 29 with compact parking (13 LDS words per lane)
-    {false, dev::STACK_LDS16, 1, 0, true, 256, false, false, 4, true}, {false, dev::STACK_LDS16, 8, 0, true, 256, false, false, 4, true},
-    // 32, 33: 13 (one wave per workgroup) with compact parking, ≤ 64 VGPRs (32) or the compiler's choice (33)
-    {false, dev::STACK_LDS16, 8, 0, true, 64, false, false, 1, true}, {false, dev::STACK_LDS16, 1, 0, true, 64, false, false, 1, true},
-    // 34: 13 over the 4-wide BVH; 35, 36: the same held to 6 / 7 waves per SIMD by registers
-    {false, dev::STACK_LDS16, 1, 0, true, 64, false, false, 1, false, true},
-    {false, dev::STACK_LDS16, 6, 0, true, 64, false, false, 1, false, true},
-    {false, dev::STACK_LDS16, 7, 0, true, 64, false, false, 1, false, true},
+    {dev::STACK_SCRATCH, 0, 256, 1, false}, {dev::STACK_LDS, 24, 64, 2, false}, {dev::STACK_LDS16, 0, 64, 3, false},
+    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4;
 
-template <bool L, int S, int W>
-KernelFn pick_count(bool count) {
-    return count ? dev::render_kernel<L, S, true, W> : dev::render_kernel<L, S, false, W>;
-}
-
-template <int W, int H = dev::NODES_48, int G = 1, bool PH = false, bool C = false>
+template <int W, bool PH = false, bool C = false>
 KernelFn v3_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v3<true, W, true, H, G, PH, C> : dev::render_kernel_v3<false, W, true, H, G, PH, C>;
-    return count ? dev::render_kernel_v3<true, W, false, H, G, PH, C> : dev::render_kernel_v3<false, W, false, H, G, PH, C>;
+    if (tex) return count ? dev::render_kernel_v3<true, W, true, PH, C> : dev::render_kernel_v3<false, W, true, PH, C>;
+    return count ? dev::render_kernel_v3<true, W, false, PH, C> : dev::render_kernel_v3<false, W, false, PH, C>;
 }
 
-template <int W, int H = dev::NODES_48, int G = 1, bool PH = false>
+template <bool PH = false>
 KernelFn v4_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v4<true, W, true, H, G, PH> : dev::render_kernel_v4<false, W, true, H, G, PH>;
-    return count ? dev::render_kernel_v4<true, W, false, H, G, PH> : dev::render_kernel_v4<false, W, false, H, G, PH>;
+    if (tex) return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH> : dev::render_kernel_v4<false, true, dev::NODES_64, PH>;
+    return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH> : dev::render_kernel_v4<false, false, dev::NODES_64, PH>;
 }
 
-// Kernels with the Philox engine (RT_FLAG_RNG_PHILOX): the v3/v4 variants the automatic choice uses.
-#ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the non-texture Philox build of variant 33
+#ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the non-texture Philox build of variant 3
 #define RT_PHILOX_COMPACT_W 1
 #endif
-constexpr int kPhiloxVariants[] = {13, 22, 25, 33};
-bool philox_capable(int variant) {
-    for (int v : kPhiloxVariants)
-        if (v == variant) return true;
-    return false;
-}
 
 KernelFn pick(int variant, bool count, bool tex, bool philox) {
-    if (philox) {
-        switch (variant) {
-        case 13: return v3_pick<1, dev::NODES_48, 1, true>(count, tex);
-        case 22: return v4_pick<1, dev::NODES_64, 1, true>(count, tex);
-        case 33:  // W = 8 (64 VGPRs, one cold 8-B spill) lost to W = 1 in a same-box A/B (c2 median 22.5-22.8
-                  // vs 21.6-21.9 ms, profiles/r01f_ab_philox_w1_w8_c2.txt); -DRT_PHILOX_COMPACT_W=8 rebuilds it
-            return tex ? v3_pick<1, dev::NODES_48, 1, true, true>(count, true)
-                       : v3_pick<RT_PHILOX_COMPACT_W, dev::NODES_48, 1, true, true>(count, false);
-        default: return v3_pick<1, dev::NODES_48, 4, true>(count, tex);  // 25
-        }
-    }
     switch (variant) {
-    case 0: return pick_count<false, dev::STACK_SCRATCH, 1>(count);
-    case 1: return pick_count<false, dev::STACK_LDS, 1>(count);
-    case 2: return pick_count<false, dev::STACK_HYBRID, 1>(count);
-    case 3: return pick_count<true, dev::STACK_SCRATCH, 1>(count);
-    case 4: return pick_count<true, dev::STACK_LDS, 1>(count);
-    case 5: return pick_count<true, dev::STACK_HYBRID, 1>(count);
-    case 6: return pick_count<false, dev::STACK_LDS, 6>(count);
-    case 7: return pick_count<false, dev::STACK_LDS, 8>(count);
-    case 8: return count ? dev::render_kernel_v2<true, 1, 256> : dev::render_kernel_v2<false, 1, 256>;
-    case 9: return count ? dev::render_kernel_v2<true, 6, 256> : dev::render_kernel_v2<false, 6, 256>;
-    case 10: return count ? dev::render_kernel_v2<true, 8, 256> : dev::render_kernel_v2<false, 8, 256>;
-    case 11: return count ? dev::render_kernel_v2<true, 1, 64> : dev::render_kernel_v2<false, 1, 64>;
-    case 12: return count ? dev::render_kernel_v2<true, 6, 64> : dev::render_kernel_v2<false, 6, 64>;
-    case 13: return v3_pick<1>(count, tex);
-    case 14: return v3_pick<6>(count, tex);
-    case 15: return v3_pick<8>(count, tex);
-    case 16: return v4_pick<1>(count, tex);
-    case 17: return v4_pick<8>(count, tex);
-    case 18: return v3_pick<1, dev::NODES_HALF>(count, tex);
-    case 19: return v4_pick<1, dev::NODES_HALF>(count, tex);
-    case 20: return v4_pick<6, dev::NODES_HALF>(count, tex);
-    case 21: return v3_pick<1, dev::NODES_64>(count, tex);
-    case 22: return v4_pick<1, dev::NODES_64>(count, tex);
-    case 24: return v3_pick<1, dev::NODES_48, 2>(count, tex);
-    case 25: return v3_pick<1, dev::NODES_48, 4>(count, tex);
-    case 26: return v4_pick<1, dev::NODES_64, 2>(count, tex);
-    case 27: return v4_pick<1, dev::NODES_64, 4>(count, tex);
-    case 28: return v3_pick<1, dev::NODES_HALF, 4>(count, tex);
-    case 29: return v3_pick<8, dev::NODES_48, 4>(count, tex);
-    case 30: return v3_pick<1, dev::NODES_48, 4, false, true>(count, tex);
-    case 31: return v3_pick<8, dev::NODES_48, 4, false, true>(count, tex);
-    case 32: return v3_pick<8, dev::NODES_48, 1, false, true>(count, tex);
-    case 33: return v3_pick<1, dev::NODES_48, 1, false, true>(count, tex);
-    case 34: return v3_pick<1, dev::NODES_W4>(count, tex);
-    case 35: return v3_pick<6, dev::NODES_W4>(count, tex);
-    case 36: return v3_pick<7, dev::NODES_W4>(count, tex);
-    default: return v4_pick<7, dev::NODES_64>(count, tex);
+    case kVarV1: return count ? dev::render_kernel<true> : dev::render_kernel<false>;
+    case kVarV2: return count ? dev::render_kernel_v2<true> : dev::render_kernel_v2<false>;
+    case kVarV3: return philox ? v3_pick<1, true>(count, tex) : v3_pick<1>(count, tex);
+    case kVarV3Compact:
+        // Philox: W = 8 (64 VGPRs, one cold 8-B spill) lost to W = 1 in a same-box A/B (c2 median 22.5-22.8
+        // vs 21.6-21.9 ms, profiles/r01f_ab_philox_w1_w8_c2.txt); -DRT_PHILOX_COMPACT_W=8 rebuilds it
+        if (philox)
+            return tex ? v3_pick<1, true, true>(count, true) : v3_pick<RT_PHILOX_COMPACT_W, true, true>(count, false);
+        return v3_pick<1, false, true>(count, tex);
+    default: return philox ? v4_pick<true>(count, tex) : v4_pick<false>(count, tex);
     }
 }
 
@@ -1919,10 +1686,17 @@ thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
+// Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
+// evicts the cache meanwhile (the buffers are freed when the last holder drops it; hipFree waits for the
+// device, so a launch still reading them completes first).
 struct TilePlan {
     uint32_t* cost = nullptr;
     uint32_t* order = nullptr;
-    bool valid = false;  // an order has been planned (by an earlier launch on the same stream)
+    std::atomic<bool> valid{false};  // an order has been planned (by an earlier launch on the same stream)
+    ~TilePlan() {
+        if (cost) (void)hipFree(cost);
+        if (order) (void)hipFree(order);
+    }
 };
 struct PlanKey {
     int device;
@@ -1935,37 +1709,27 @@ struct PlanKey {
         return tiles < o.tiles;
     }
 };
-std::map<PlanKey, TilePlan> g_plans;
+std::map<PlanKey, std::shared_ptr<TilePlan>> g_plans;
 std::mutex g_plans_mu;
 constexpr size_t kMaxPlans = 32;
 
-int acquire_plan(const PlanKey& key, hipStream_t s, TilePlan** out) {
+int acquire_plan(const PlanKey& key, hipStream_t s, std::shared_ptr<TilePlan>* out) {
     std::lock_guard<std::mutex> lock(g_plans_mu);
     auto it = g_plans.find(key);
     if (it == g_plans.end()) {
-        if (g_plans.size() >= kMaxPlans) {  // drop every plan (hipFree waits for the device)
-            for (auto& kv : g_plans) {
-                (void)hipFree(kv.second.cost);
-                (void)hipFree(kv.second.order);
-            }
-            g_plans.clear();
-        }
-        TilePlan p;
+        if (g_plans.size() >= kMaxPlans) g_plans.clear();  // holders keep their plans alive
+        auto p = std::make_shared<TilePlan>();
         void* c = nullptr;
         void* o = nullptr;
         int rc = hip_check(hipMalloc(&c, (size_t)key.tiles * 4), "rt_render: tile cost allocation");
+        p->cost = (uint32_t*)c;
         if (rc == RT_OK) rc = hip_check(hipMalloc(&o, (size_t)key.tiles * 4), "rt_render: tile order allocation");
+        p->order = (uint32_t*)o;
         if (rc == RT_OK) rc = hip_check(hipMemsetAsync(c, 0, (size_t)key.tiles * 4, s), "rt_render: tile cost reset");
-        if (rc != RT_OK) {
-            if (c) (void)hipFree(c);
-            if (o) (void)hipFree(o);
-            return rc;
-        }
-        p.cost = (uint32_t*)c;
-        p.order = (uint32_t*)o;
-        it = g_plans.emplace(key, p).first;
+        if (rc != RT_OK) return rc;
+        it = g_plans.emplace(key, std::move(p)).first;
     }
-    *out = &it->second;
+    *out = it->second;
     return RT_OK;
 }
 thread_local int g_persistent_waves = 0;  // 0: occupancy query
@@ -2035,8 +1799,7 @@ int rt_set_timing(int enabled) {
 
 float rt_last_kernel_ms(void) { return g_last_ms; }
 
-// Benchmark/tuning knob: -1 = automatic; 0..5 = (scene in LDS) * 3 + stack kind (0 scratch, 1 LDS,
-// 2 registers + scratch).  Returns the previous value.
+// Benchmark/tuning knob: -1 = automatic, else an index into kVariants.  Returns the previous value.
 int rt_set_variant(int variant) {
     int prev = g_variant;
     g_variant = variant;
@@ -2132,9 +1895,6 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.nodes = (const float4*)S.nodes;
     P.nodes48 = (const float4*)S.nodes48;
     P.refs16 = (const uint32_t*)S.refs16;
-    P.nodes_w4 = (const float*)S.nodes_w4;
-    P.num_nodes_w4 = S.num_nodes_w4;
-    P.nodes32 = (const uint32_t*)S.nodes32;
     P.prims = (const float4*)S.prims;
     P.mats = (const float4*)S.mats;
     P.imgs = (const int4*)S.imgs;
@@ -2203,34 +1963,39 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
 
     const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
-    const size_t scene_lds = (size_t)S.num_nodes * 64 + (size_t)S.num_prims * 32;
     int variant = g_variant;
     // auto: the fastest measured kernel per workload shape (profiles/r01d_*, r01e_*): the persistent v4 when a
     // pixel has few paths (config 5: 1 spp, 0.51-0.54 vs 0.80 ms), otherwise v3 with the adaptive
-    // longest-first tile order and compact parking (33): 13 words of parked state + a depth + 2 stack fit
-    // config 2's wave in 5 KB of LDS, 8 waves per SIMD (config 2: 17.05 vs 17.8 ms for 13; config 3, depth
-    // 16: 365 vs 408 ms for v4).  33 falls back to 13 where the packed counters would overflow.
+    // longest-first tile order and compact parking: 13 words of parked state + a depth + 2 stack fit config
+    // 2's wave in 5 KB of LDS, 8 waves per SIMD (config 2: 17.05 vs 17.8 ms with 15-word parking; config 3,
+    // depth 16: 365 vs 408 ms for v4).  Compact parking falls back to 15 words where its packed counters
+    // would overflow.
     if (variant < 0 || variant >= kNumVariants)
-        variant = a->samples_per_pixel < 32 ? 22 : 33;
-    if (kVariants[variant].stack == dev::STACK_LDS16 && (S.num_nodes >= (uint32_t)dev::kSentinel16 || S.num_prims >= 8192u))
-        variant = S.depth <= 25u ? 11 : 0;  // 16-bit references do not fit: 32-bit LDS stacks, or scratch if deep
-    if (kVariants[variant].half && !S.has_half_nodes)  // a plane beyond the binary16 range: f32 boxes
-        variant = variant == 18 ? 13 : (variant == 19 ? 16 : (variant == 28 ? 25 : 17));
-    if (kVariants[variant].compact &&
-        !(a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u))
-        variant = variant == 30 ? 25 : (variant == 31 ? 29 : (variant == 32 ? 15 : 13));  // packed counters would overflow
-    if (kVariants[variant].w4 && (S.num_nodes_w4 == 0 || S.num_nodes_w4 >= (uint32_t)dev::kSentinel16))
-        variant = 13;  // no 4-wide tree (empty scene) or its references do not fit 16 bits
-    if (kVariants[variant].persistent && (a->samples_per_pixel == 0 || a->max_depth == 0))
-        variant = kVariants[variant].half ? 18 : 13;  // the persistent kernel assumes every pixel traces a ray
-    if (philox && !philox_capable(variant)) {
-        if (kVariants[variant].stack != dev::STACK_LDS16) {
+        variant = a->samples_per_pixel < 32 ? kVarV4 : kVarV3Compact;
+    const bool refs16_fit = S.num_nodes < (uint32_t)dev::kSentinel16 && S.num_prims < 8192u;
+    if (kVariants[variant].stack == dev::STACK_LDS16 && !refs16_fit) {
+        if (philox) {
             set_error("rt_render: RT_FLAG_RNG_PHILOX needs the v3/v4 kernels (< 32767 BVH nodes, < 8192 primitives)");
             return RT_ERR_UNSUPPORTED;
         }
-        variant = kVariants[variant].persistent ? 22 : 13;
+        variant = S.depth <= 25u ? kVarV2 : kVarV1;  // 32-bit LDS stacks, or scratch if deep
+    }
+    if (kVariants[variant].compact &&
+        !(a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u))
+        variant = kVarV3;  // packed counters would overflow
+    if (kVariants[variant].kernel == 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
+        variant = kVarV3;  // the persistent kernel assumes every pixel traces a ray
+    if (philox && kVariants[variant].stack != dev::STACK_LDS16) {
+        if (!refs16_fit) {
+            set_error("rt_render: RT_FLAG_RNG_PHILOX needs the v3/v4 kernels (< 32767 BVH nodes, < 8192 primitives)");
+            return RT_ERR_UNSUPPORTED;
+        }
+        variant = kVarV3Compact;  // the v1/v2 fallbacks have no Philox build
+        if (!(a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u))
+            variant = kVarV3;
     }
     const Variant& V = kVariants[variant];
+    const bool persistent = V.kernel == 4;
     // near-first traversal holds at most one deferred child per level below the root
     if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
@@ -2239,26 +2004,24 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // v3/v4: per wave, the parked path state + a 16-bit stack of depth + 2 entries: two sentinel pads, and
     // a visit at level L (root = 1) holds at most L - 1 deferred children, so its unconditional write of
     // the far child lands at index 2 + (L - 1) <= depth + 1 (the 128-B saving keeps config 2's wave
-    // inside 11 × 512 B of LDS)
+    // inside 10 × 512 B of LDS)
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
-                                  ? (size_t)(V.persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
-                                        (size_t)(V.w4 ? S.stack_w4 + 5 : S.depth + 2) * 64 * 2 +
-                                        (size_t)g_lds_pad
+                                  ? (size_t)(persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
+                                        (size_t)(S.depth + 2) * 64 * 2 + (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
-    size_t lds_bytes = (V.scene_lds ? scene_lds : 0) +
-                       (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes * (size_t)V.wpg;
+    size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes;
     if (lds_bytes > kLdsLimit) {
-        set_error("rt_render: scene does not fit in LDS for this variant");
+        set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
     }
     KernelFn fn = pick(variant, count_tests, S.has_textures, philox);
-    const uint32_t tile = (V.block == 64 || V.wpg > 1) ? 8u : 16u;  // v3/v4: one 8×8 tile per wave
+    const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave
     P.tiles_x = (a->width + tile - 1) / tile;
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
     hipStream_t s = (hipStream_t)stream;
-    uint32_t grid = (tiles + (uint32_t)V.wpg - 1) / (uint32_t)V.wpg;
-    if (V.persistent) {
+    uint32_t grid = tiles;
+    if (persistent) {
         int device = 0, cus = 0, per_cu = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
         if (rc == RT_OK) rc = acquire_queue(device, &P.work_counter, &cus);
@@ -2274,14 +2037,14 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         if (rc != RT_OK) return rc;
     }
     P.num_tiles = tiles;
-    TilePlan* plan = nullptr;
-    if (V.stack == dev::STACK_LDS16 && !V.persistent && g_adaptive_order && !g_tile_order) {
+    std::shared_ptr<TilePlan> plan;
+    if (V.kernel == 3 && g_adaptive_order && !g_tile_order) {
         int device = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
         if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles}, s, &plan);
         if (rc != RT_OK) return rc;
         P.tile_cost = plan->cost;
-        P.tile_order = plan->valid ? plan->order : nullptr;
+        P.tile_order = plan->valid.load() ? plan->order : nullptr;
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing) {
@@ -2296,7 +2059,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         hipLaunchKernelGGL(dev::plan_order_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)plan->cost, plan->order,
                            tiles);
         rc = hip_check(hipGetLastError(), "rt_render: plan kernel launch", RT_ERR_LAUNCH);
-        if (rc == RT_OK) plan->valid = true;
+        if (rc == RT_OK) plan->valid.store(true);
     }
     if (g_timing) {
         (void)hipEventRecord(e1, s);

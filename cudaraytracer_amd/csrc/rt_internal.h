@@ -43,14 +43,6 @@ struct HostScene {
     std::vector<float> nodes;   // 16 floats per node
     std::vector<float> nodes48; // 12 floats per node: the three box float4 of `nodes` (v3 kernels)
     std::vector<uint32_t> refs16;  // per node: child 0 | child 1 << 16 as signed 16-bit references
-    std::vector<uint32_t> nodes32; // 8 words per node: binary16 child boxes + refs16 (HALF kernels)
-    bool has_half_nodes = false;   // every plane representable as a finite binary16 (rounded outward)
-    // 4-wide BVH (v3 NODES_W4 kernels), collapsed from the binary one: per node 4 child boxes
-    // (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z; unused slots empty) then 4 16-bit references (26 words)
-    std::vector<float> nodes_w4;
-    uint32_t num_nodes_w4 = 0;
-    uint32_t depth_w4 = 0;         // max root-to-leaf 4-wide node count
-    uint32_t stack_w4 = 0;         // max over root-to-leaf paths of the entries the traversal defers
     std::vector<float> prims;   // 8 floats per primitive
     std::vector<float> mats;    // 12 floats per material
     std::vector<int32_t> imgs;  // 4 ints per image

@@ -11,16 +11,12 @@ struct DeviceScene {
     const void* nodes = nullptr;   // float4 × 4 per node
     const void* nodes48 = nullptr; // float4 × 3 per node (boxes only)
     const void* refs16 = nullptr;  // uint32 per node: two signed 16-bit child references
-    const void* nodes32 = nullptr; // 32 B per node: binary16 child boxes + packed references
-    const void* nodes_w4 = nullptr; // 104 B per node: 4 child boxes + 4 16-bit references
-    uint32_t num_nodes_w4 = 0, depth_w4 = 0, stack_w4 = 0;
     const void* prims = nullptr;   // float4 × 2 per primitive
     const void* mats = nullptr;    // float4 × 3 per material
     const void* imgs = nullptr;    // int4 per image
     const void* texels = nullptr;  // RGB8
     uint32_t num_nodes = 0, num_prims = 0, num_mats = 0, depth = 0;
     bool has_image_textures = false;
-    bool has_half_nodes = false;
     bool has_textures = false;  // any CHECKER or IMAGE albedo (selects the texture-capable kernel)
     uint64_t device_bytes = 0;
 };

@@ -53,37 +53,6 @@ RectGeom rect_geom(const rt_hittable_desc& h) {
     return g;
 }
 
-// binary16 helpers (host only, no _Float16 dependency).  Ordered key of a finite half: monotone in its
-// value (keys -0x7bff..0x7bff; +0 and -0 both map to 0).
-float half_value(int key) {
-    const uint32_t m = (uint32_t)(key < 0 ? -key : key);
-    const uint32_t e = m >> 10, f = m & 0x3ffu;
-    const float mag = e == 0 ? std::ldexp((float)f, -24) : std::ldexp((float)(1024u + f), (int)e - 25);
-    return key < 0 ? -mag : mag;
-}
-uint16_t half_bits(int key) { return key < 0 ? (uint16_t)(0x8000u | (uint32_t)(-key)) : (uint16_t)key; }
-
-// Largest finite binary16 <= v, as bits, or -1 if there is none (v < -65504 or NaN).
-int half_round_down(float v) {
-    if (!(v >= -65504.0f)) return -1;
-    int lo = -0x7bff, hi = 0x7bff;  // invariant: half_value(lo) <= v
-    while (lo < hi) {
-        const int mid = lo + (hi - lo + 1) / 2;
-        if (half_value(mid) <= v) lo = mid; else hi = mid - 1;
-    }
-    return half_bits(lo);
-}
-// Smallest finite binary16 >= v, as bits, or -1 if there is none.
-int half_round_up(float v) {
-    if (!(v <= 65504.0f)) return -1;
-    int lo = -0x7bff, hi = 0x7bff;  // invariant: half_value(hi) >= v
-    while (lo < hi) {
-        const int mid = lo + (hi - lo) / 2;
-        if (half_value(mid) >= v) hi = mid; else lo = mid + 1;
-    }
-    return half_bits(lo);
-}
-
 // Reference primitive box (Hittable.cuh:112-116, 171-181, 227-237, 283-293), grown outward.
 Box prim_box(const rt_hittable_desc& h) {
     Box b;
@@ -198,86 +167,12 @@ struct Builder {
     }
 };
 
-// 4-wide BVH from the binary one: each 4-wide node takes a binary node's two children and repeatedly
-// opens the internal child with the largest surface area until it holds four children or only leaves
-// (the usual collapse; the traversal then needs half as many dependent node fetches per ray).  Leaf
-// references are the binary tree's; internal references are 4-wide node indices (pre-order, root 0).
-void collapse_w4(const Builder& B, HostScene* out) {
-    out->nodes_w4.clear();
-    out->num_nodes_w4 = 0;
-    out->depth_w4 = 0;
-    out->stack_w4 = 0;
-    if (B.nodes.empty()) return;
-    struct Slot { Box box; int ref; };
-    std::vector<std::array<Slot, 4>> w4;
-    std::vector<int> count;
-    uint32_t max_depth = 0;
-    std::function<int(int, uint32_t)> make = [&](int bin, uint32_t depth) -> int {
-        std::array<Slot, 4> s;
-        int n = 2;
-        s[0] = {B.nodes[bin].box[0], B.nodes[bin].child[0]};
-        s[1] = {B.nodes[bin].box[1], B.nodes[bin].child[1]};
-        while (n < 4) {
-            int best = -1;
-            float best_area = -1.0f;
-            for (int i = 0; i < n; i++)
-                if (s[i].ref >= 0 && s[i].box.area() > best_area) { best = i; best_area = s[i].box.area(); }
-            if (best < 0) break;
-            const Builder::Node& c = B.nodes[s[best].ref];
-            s[best] = {c.box[0], c.child[0]};
-            s[n++] = {c.box[1], c.child[1]};
-        }
-        const int id = (int)w4.size();
-        w4.push_back(s);
-        count.push_back(n);
-        max_depth = std::max(max_depth, depth);
-        for (int i = 0; i < n; i++)
-            if (w4[id][i].ref >= 0) {
-                const int child = make(w4[id][i].ref, depth + 1);
-                w4[id][i].ref = child;
-            }
-        return id;
-    };
-    make(0, 1);
-    // deepest stack: a visit defers at most (children - 1) entries, so the bound is the largest sum of
-    // (children - 1) along a root-to-leaf path (children precede parents in reverse pre-order)
-    std::vector<uint32_t> defer(w4.size(), 0);
-    for (size_t i = w4.size(); i-- > 0;) {
-        uint32_t below = 0;
-        for (int c = 0; c < count[i]; c++)
-            if (w4[i][c].ref >= 0) below = std::max(below, defer[(size_t)w4[i][c].ref]);
-        defer[i] = (uint32_t)(count[i] - 1) + below;
-    }
-    out->stack_w4 = defer[0];
-    out->num_nodes_w4 = (uint32_t)w4.size();
-    out->depth_w4 = max_depth;
-    out->nodes_w4.assign((size_t)out->num_nodes_w4 * 26, 0.0f);
-    for (size_t i = 0; i < w4.size(); i++) {
-        float* o = out->nodes_w4.data() + i * 26;
-        uint16_t refs[4];
-        for (int c = 0; c < 4; c++) {
-            if (c < count[i]) {
-                const Box& b = w4[i][c].box;
-                o[6 * c + 0] = b.lo[0]; o[6 * c + 1] = b.hi[0];
-                o[6 * c + 2] = b.lo[1]; o[6 * c + 3] = b.hi[1];
-                o[6 * c + 4] = b.lo[2]; o[6 * c + 5] = b.hi[2];
-                refs[c] = (uint16_t)((uint32_t)w4[i][c].ref & 0xffffu);  // valid when refs fit int16
-            } else {  // empty slot: lo > hi on every axis, so the slab test never reports a hit
-                for (int a = 0; a < 3; a++) { o[6 * c + 2 * a] = 3e38f; o[6 * c + 2 * a + 1] = -3e38f; }
-                refs[c] = 0x7fffu;
-            }
-        }
-        o[24] = bits_to_float((uint32_t)refs[0] | ((uint32_t)refs[1] << 16));
-        o[25] = bits_to_float((uint32_t)refs[2] | ((uint32_t)refs[3] << 16));
-    }
-}
-
 int check_texture(const rt_texture_desc& t, uint32_t num_images, std::string* err) {
     if (t.type < RT_CONSTANT || t.type > RT_IMAGE) {
         *err = "texture type " + std::to_string(t.type) + " is not CONSTANT/CHECKER/IMAGE";
         return RT_ERR_INVALID_SCENE;
     }
-    if (t.type == RT_IMAGE && t.image >= (int32_t)num_images) {
+    if (t.type == RT_IMAGE && (t.image < -1 || t.image >= (int32_t)num_images)) {
         *err = "image texture index " + std::to_string(t.image) + " out of range";
         return RT_ERR_INVALID_SCENE;
     }
@@ -346,15 +241,25 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         if (desc->materials[i].type != RT_DIELECTRIC && desc->materials[i].albedo.type != RT_CONSTANT)
             out->has_textures = true;
 
-    // images
+    // images: RGB8, 3 bytes per texel (Texture.cuh:76); data == NULL means "no data" (Texture.cuh:83-84)
     size_t off = 0;
     for (uint32_t i = 0; i < desc->num_images; i++) {
         const rt_image_desc& im = desc->images[i];
-        if (im.width < 0 || im.height < 0 || (im.data == nullptr && im.width * im.height != 0)) {
-            // data == NULL is allowed and means "no data" (Texture.cuh:83-84) when w·h == 0
+        if (im.width < 0 || im.height < 0) {
+            *err = "image " + std::to_string(i) + ": negative width or height";
+            return RT_ERR_INVALID_SCENE;
         }
-        size_t bytes = im.data ? (size_t)im.width * (size_t)im.height * 3 : 0;
-        out->imgs.push_back(im.data ? (int32_t)off : -1);
+        const uint64_t texels = (uint64_t)im.width * (uint64_t)im.height;
+        if (im.data && texels > (uint64_t)1 << 31) {  // the kernel indexes texel bytes with 64-bit offsets
+            *err = "image " + std::to_string(i) + ": more than 2^31 texels";
+            return RT_ERR_INVALID_SCENE;
+        }
+        const size_t bytes = im.data ? (size_t)texels * 3 : 0;
+        if (bytes && off + bytes > (size_t)INT32_MAX) {  // imgs[] holds 32-bit byte offsets
+            *err = "images exceed 2 GiB of texels in one scene";
+            return RT_ERR_INVALID_SCENE;
+        }
+        out->imgs.push_back(bytes ? (int32_t)off : -1);
         out->imgs.push_back(im.width);
         out->imgs.push_back(im.height);
         out->imgs.push_back(0);
@@ -410,33 +315,6 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         const Builder::Node& n = B.nodes[i];
         out->refs16[i] = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);  // valid when refs fit int16
     }
-    // binary16 child boxes (v3/v4 HALF kernels): planes rounded outward, so the box still contains the
-    // padded fp32 box and culling stays conservative; only when every plane is a finite binary16
-    out->has_half_nodes = true;
-    out->nodes32.assign((size_t)out->num_nodes * 8, 0u);
-    for (uint32_t i = 0; i < out->num_nodes && out->has_half_nodes; i++) {
-        const Builder::Node& n = B.nodes[i];
-        uint32_t* o = out->nodes32.data() + (size_t)i * 8;
-        uint16_t h[2][3][2];
-        for (int c = 0; c < 2; c++)
-            for (int a = 0; a < 3; a++) {
-                int lo = half_round_down(n.box[c].lo[a]), hi = half_round_up(n.box[c].hi[a]);
-                if (lo < 0 || hi < 0) {
-                    out->has_half_nodes = false;
-                    break;
-                }
-                h[c][a][0] = (uint16_t)lo;
-                h[c][a][1] = (uint16_t)hi;
-            }
-        if (!out->has_half_nodes) break;
-        auto pack = [](const uint16_t* lohi) { return (uint32_t)lohi[0] | ((uint32_t)lohi[1] << 16); };
-        o[0] = pack(h[0][0]); o[1] = pack(h[0][1]); o[2] = pack(h[1][0]); o[3] = pack(h[1][1]);
-        o[4] = pack(h[0][2]); o[5] = pack(h[1][2]);
-        o[6] = out->refs16[i];
-        o[7] = 0u;
-    }
-    if (!out->has_half_nodes) out->nodes32.clear();
-    collapse_w4(B, out);
     out->prims.resize((size_t)out->num_prims * 8);
     out->prim_source.resize(out->num_prims);
     for (uint32_t i = 0; i < out->num_prims; i++) {

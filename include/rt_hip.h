@@ -304,14 +304,6 @@ typedef struct rt_host_tables_info {
 int rt_build_host_tables(const rt_scene_desc* desc, float* nodes, float* prims, float* materials,
                          int32_t* prim_source, rt_host_tables_info* info);
 
-/* The 32-B binary16 BVH nodes the HALF kernels read (8 words per node, same topology as `nodes` above):
- *   w0..w1 = child 0 x/y planes, w2..w3 = child 1 x/y planes, w4 = child 0 z, w5 = child 1 z
- *   (each word = lo | hi << 16 as binary16, lo rounded down and hi rounded up from the fp32 plane),
- *   w6 = child 0 | child 1 << 16 (signed 16-bit references), w7 = 0.
- * RT_ERR_UNSUPPORTED when a plane lies beyond the binary16 range (the kernels then use fp32 boxes).
- * Size query with NULL nodes32.  Test/inspection helper; not part of the reference interface. */
-int rt_build_host_half_nodes(const rt_scene_desc* desc, uint32_t* nodes32, uint32_t* num_nodes);
-
 /* glibc random_r TYPE_3 restatement: rand() sequence after srand(seed) (RND macro, Math.cuh:12). */
 typedef struct rt_glibc_rand { int32_t r[34]; uint32_t idx; } rt_glibc_rand;
 void rt_glibc_srand(rt_glibc_rand* g, uint32_t seed);

@@ -481,7 +481,11 @@ static v3 texture_value(const orc_scene* s, const rt_texture_desc* t, float u, f
         return sines < 0 ? ld3(t->color) : ld3(t->color2);
     }
     case RT_IMAGE: { /* Image::value :83-105 */
-        if (t->image < 0 || t->image >= s->nimages || !s->images[t->image].data) return mk(0.0f, 1.0f, 1.0f);
+        /* data == nullptr → cyan (:83-84).  Documented deviation: an image with data but no texels (w·h == 0)
+           is also cyan; the reference would read data[-3] (i = width - 1 = -1, :88-91), undefined. */
+        if (t->image < 0 || t->image >= s->nimages || !s->images[t->image].data || s->images[t->image].width <= 0 ||
+            s->images[t->image].height <= 0)
+            return mk(0.0f, 1.0f, 1.0f);
         const rt_image_desc* im = &s->images[t->image];
         u = fclampf(u, 0.0f, 1.0f);
         v = 1.0f - fclampf(v, 0.0f, 1.0f);

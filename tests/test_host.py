@@ -192,40 +192,3 @@ def test_reference_graph_rejects_non_bvh_world():
     nh, nm, ni = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
     assert lib().rt_reference_graph_flatten(C.addressof(bad), None, C.byref(nh), None, C.byref(nm), None,
                                             C.byref(ni)) == -2
-
-
-@pytest.mark.parametrize("which", range(5))
-def test_half_nodes_contain_the_fp32_boxes_and_are_tight(which):
-    """The binary16 node layout of the HALF kernels: same references, every plane rounded outward to the
-    nearest binary16 (lo <= fp32 lo < next half up; hi >= fp32 hi > next half down)."""
-    scene = scenes.builtin(which)
-    info, nodes, _, _ = _tables(scene)
-    desc = scene.desc()
-    n = C.c_uint32()
-    assert lib().rt_build_host_half_nodes(C.byref(desc), None, C.byref(n)) == 0
-    assert n.value == info.num_nodes
-    buf = (C.c_uint32 * (8 * n.value))()
-    assert lib().rt_build_host_half_nodes(C.byref(desc), buf, C.byref(n)) == 0
-    words = np.frombuffer(buf, np.uint32).reshape(-1, 8)
-    halves = words[:, :6].copy().view(np.float16).reshape(-1, 12).astype(np.float32)  # lo, hi pairs
-    # fp32 planes in the same order: c0.x c0.y c1.x c1.y c0.z c1.z as (lo, hi)
-    f32 = nodes[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]]
-    lo_h, hi_h = halves[:, 0::2], halves[:, 1::2]
-    lo_f, hi_f = f32[:, 0::2], f32[:, 1::2]
-    assert np.all(lo_h <= lo_f) and np.all(hi_h >= hi_f)
-    up = np.nextafter(lo_h.astype(np.float16), np.float16(np.inf)).astype(np.float32)
-    dn = np.nextafter(hi_h.astype(np.float16), np.float16(-np.inf)).astype(np.float32)
-    assert np.all(up > lo_f) and np.all(dn < hi_f)
-    ints = nodes.view(np.int32)
-    refs = words[:, 6]
-    np.testing.assert_array_equal((refs & 0xFFFF).astype(np.uint16).view(np.int16), ints[:, 12].astype(np.int16))
-    np.testing.assert_array_equal((refs >> 16).astype(np.uint16).view(np.int16), ints[:, 13].astype(np.int16))
-    assert np.all(words[:, 7] == 0)
-
-
-def test_half_nodes_unsupported_beyond_binary16_range():
-    scene = scenes.builtin(1)
-    scene.hittables[0].center[0] = 70000.0
-    desc = scene.desc()
-    n = C.c_uint32()
-    assert lib().rt_build_host_half_nodes(C.byref(desc), None, C.byref(n)) == -6  # RT_ERR_UNSUPPORTED

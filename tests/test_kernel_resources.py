@@ -2,9 +2,9 @@
 
 A private array that LLVM materialises in scratch (it happened to the Philox word select: scratch loads on
 every draw, +8 % frame time) or a register count past 72 (7 waves per SIMD) is a performance regression
-the parity tests cannot see.  This test pins "no scratch" for the v3 (variant 13) and v4 (variant 22)
+the parity tests cannot see.  This test pins "no scratch" for the v3 (variants 2, 3) and v4 (variant 4)
 kernels in both RNG modes, with and without texture support, and <= 72 VGPRs for the v3 kernels of
-untextured scenes (<= 64 for the XORWOW build of 33, the headline kernel; the texture-capable and persistent kernels run at 85-98
+untextured scenes (<= 64 for the XORWOW build of variant 3, the headline kernel; the texture-capable and persistent kernels run at 85-98
 VGPRs, 5 waves per SIMD, measured in DESIGN.md)."""
 import os
 import re
@@ -17,11 +17,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "cudaraytracer_amd", "librt_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
-# render_kernel_v3<COUNT_TESTS=false, W=1, TEX, NODES_48=0, WPG=1, PHILOX, COMPACT> (variants 13 and 33)
-# render_kernel_v4<COUNT_TESTS=false, W=1, TEX, NODES_64=2, WPG=1, PHILOX>
-HOT = [f"_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb{t}ELi0ELi1ELb{p}ELb{c}EEEvNS0_7KParamsE"
+# render_kernel_v3<COUNT_TESTS=false, W=1, TEX, PHILOX, COMPACT> (variants 2 and 3)
+# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX> (variant 4)
+HOT = [f"_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb{t}ELb{p}ELb{c}EEEvNS0_7KParamsE"
        for t in (0, 1) for p in (0, 1) for c in (0, 1)] + \
-      [f"_ZN2rt3dev16render_kernel_v4ILb0ELi1ELb{t}ELi2ELi1ELb{p}EEEvNS0_7KParamsE" for t in (0, 1) for p in (0, 1)]
+      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}EEEvNS0_7KParamsE" for t in (0, 1) for p in (0, 1)]
 
 
 def kernel_metadata(tmp_path):
@@ -54,5 +54,5 @@ def test_hot_kernels_use_no_scratch_and_at_most_72_vgprs(tmp_path):
         assert meta[k]["vgpr_spill_count"] == 0, (k, meta[k])
         if "render_kernel_v3ILb0ELi1ELb0E" in k:
             assert meta[k]["vgpr_count"] <= 72, (k, meta[k])
-    # the default kernel of untextured many-sample frames (variant 33, XORWOW) at 8 waves per SIMD
-    assert meta["_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb0ELi0ELi1ELb0ELb1EEEvNS0_7KParamsE"]["vgpr_count"] <= 64
+    # the default kernel of untextured many-sample frames (variant 3, XORWOW) at 8 waves per SIMD
+    assert meta["_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb0ELb0ELb1EEEvNS0_7KParamsE"]["vgpr_count"] <= 64
