@@ -38,6 +38,7 @@ EXPORTED = [
     "rt_glibc_rand_next",
     "rt_builtin_scene",
     "rt_camera_inputs",
+    "rt_procedural_texture",
     "rt_reference_graph_flatten",
     "rt_build_host_tables",
 ]
@@ -73,6 +74,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_glibc_rand_next.restype = C.c_int32
     lib.rt_builtin_scene.argtypes = [C.c_int, C.c_uint32, P(abi.HittableDesc), P(C.c_uint32),
                                      P(abi.MaterialDesc), P(C.c_uint32)]
+    lib.rt_procedural_texture.argtypes = [C.c_int, C.c_int32, C.c_int32, C.c_void_p]
     F3P = P(C.c_float)
     lib.rt_camera_inputs.argtypes = [F3P, F3P, F3P, C.c_float, C.c_float, C.c_float, F3P, F3P, P(abi.InputStruct)]
     lib.rt_reference_graph_flatten.argtypes = [vp, P(abi.HittableDesc), P(C.c_uint32), P(abi.MaterialDesc),

@@ -8,8 +8,11 @@
 // Where the reference's C++ leaves the evaluation order of several RND calls in one expression
 // unspecified (e.g. `Vec3(a + RND, 0.2f, b + RND)`, CudaLayer.cpp:201), the draws here are taken left to
 // right; the generated scenes are inputs, committed as fixtures under tests/golden/.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "rt_internal.h"
 
@@ -218,7 +221,9 @@ void cornell(SceneOut& s) {
     s.add_hittable(RT_SPHERE, 370.0f, 120.0f, 370.0f, 120.0f, 0, 0, alu);
 }
 
-// BASELINE config 5: textured spheres (image 0 is supplied by the caller) over a checker ground.
+// BASELINE config 5: textured spheres over a checker ground.  Images 0, 1, 2 are supplied by the caller (the
+// reference's 8192×4096 planet textures, assets/textures/8k_*.jpg, or rt_procedural_texture stand-ins):
+// an "earth" and a "moon" Lambertian sphere and an emissive "sun" (DiffuseLight with an Image texture).
 void textured(SceneOut& s) {
     rt_material_desc ground;
     std::memset(&ground, 0, sizeof(ground));
@@ -234,17 +239,122 @@ void textured(SceneOut& s) {
     img.albedo.type = RT_IMAGE;
     img.albedo.image = 0;
     int earth = s.add_material(img);
+    rt_material_desc moon_m = img;
+    moon_m.albedo.image = 1;
+    int moon = s.add_material(moon_m);
     rt_material_desc glow = img;
     glow.type = RT_DIFFUSELIGHT;
     glow.light_intensity = 2;
+    glow.albedo.image = 2;
     int lamp = s.add_material(glow);
     s.add_hittable(RT_SPHERE, 0.0f, 1.0f, 0.0f, 1.5f, 0, 0, earth);
-    s.add_hittable(RT_SPHERE, -3.5f, 0.5f, 0.5f, 1.0f, 0, 0, earth);
+    s.add_hittable(RT_SPHERE, -3.5f, 0.5f, 0.5f, 1.0f, 0, 0, moon);
     s.add_hittable(RT_SPHERE, 3.5f, 0.7f, -0.5f, 1.2f, 0, 0, lamp);
     s.add_hittable(RT_SPHERE, 1.5f, 0.0f, 2.5f, 0.5f, 0, 0, s.add_material(metal(0.8f, 0.8f, 0.8f, 0.05f)));
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Procedural RGB8 textures standing in for the reference's 8K planet maps (assets/textures/8k_*.jpg; this
+// image has no JPEG decoder).  Every texel is a pure function of (kind, x, y, width, height): fractal value
+// noise over an integer hash lattice, so tests and benchmarks regenerate identical bytes anywhere.
+// ---------------------------------------------------------------------------------------------------
+inline uint32_t lattice_hash(uint32_t x, uint32_t y, uint32_t seed) {
+    uint32_t h = x * 0x8da6b343u ^ y * 0xd8163841u ^ seed * 0xcb1ab31fu;
+    h ^= h >> 15;
+    h *= 0x2c1b3c6du;
+    h ^= h >> 12;
+    h *= 0x297a2d39u;
+    h ^= h >> 15;
+    return h;
+}
+
+float value_noise(float x, float y, uint32_t seed) {
+    const float fx0 = std::floor(x), fy0 = std::floor(y);
+    const uint32_t ix = (uint32_t)(int32_t)fx0, iy = (uint32_t)(int32_t)fy0;
+    float fx = x - fx0, fy = y - fy0;
+    fx = fx * fx * (3.0f - 2.0f * fx);
+    fy = fy * fy * (3.0f - 2.0f * fy);
+    const float k = 1.0f / 16777216.0f;
+    const float a = (float)(lattice_hash(ix, iy, seed) >> 8) * k, b = (float)(lattice_hash(ix + 1, iy, seed) >> 8) * k;
+    const float c = (float)(lattice_hash(ix, iy + 1, seed) >> 8) * k, d = (float)(lattice_hash(ix + 1, iy + 1, seed) >> 8) * k;
+    return (a + (b - a) * fx) + ((c + (d - c) * fx) - (a + (b - a) * fx)) * fy;
+}
+
+float fbm(float x, float y, uint32_t seed, int octaves) {
+    float sum = 0.0f, amp = 0.5f, norm = 0.0f;
+    for (int o = 0; o < octaves; o++) {
+        sum += amp * value_noise(x, y, seed + (uint32_t)o * 101u);
+        norm += amp;
+        amp *= 0.5f;
+        x *= 2.03f;
+        y *= 2.03f;
+    }
+    return sum / norm;
+}
+
+inline uint8_t to_u8(float v) { return (uint8_t)(v < 0.0f ? 0.0f : (v > 255.0f ? 255.0f : v)); }
+
+void texture_rows(int kind, int32_t w, int32_t h, uint8_t* rgb, int32_t y0, int32_t y1) {
+    for (int32_t y = y0; y < y1; y++) {
+        const float v = ((float)y + 0.5f) / (float)h;  // 0 at the top row (stb loads top-down)
+        const float lat = std::fabs(v - 0.5f) * 2.0f;  // 0 at the equator, 1 at the poles
+        for (int32_t x = 0; x < w; x++) {
+            const float u = ((float)x + 0.5f) / (float)w;
+            uint8_t* px = rgb + ((size_t)y * (size_t)w + (size_t)x) * 3;
+            float r, g, b;
+            if (kind == 0) {  // earth: oceans, continents, deserts, ice caps
+                const float n = fbm(u * 12.0f, v * 6.0f, 7u, 6);
+                const float m = fbm(u * 40.0f, v * 20.0f, 19u, 3);
+                if (lat > 0.86f + 0.08f * (m - 0.5f)) {
+                    r = 235.0f; g = 240.0f; b = 250.0f;
+                } else if (n > 0.53f) {
+                    const float dry = fbm(u * 25.0f, v * 12.0f, 31u, 4);
+                    r = 60.0f + 120.0f * dry; g = 110.0f + 50.0f * (1.0f - dry); b = 40.0f + 30.0f * m;
+                } else {
+                    r = 15.0f + 20.0f * m; g = 45.0f + 40.0f * n; b = 120.0f + 80.0f * n;
+                }
+            } else if (kind == 1) {  // moon: grey highlands, dark maria, crater speckle
+                const float n = fbm(u * 16.0f, v * 8.0f, 43u, 6);
+                const float c = fbm(u * 90.0f, v * 45.0f, 59u, 2);
+                float l = 90.0f + 110.0f * n - (n < 0.45f ? 45.0f : 0.0f) - (c > 0.7f ? 50.0f * (c - 0.7f) / 0.3f : 0.0f);
+                r = l; g = l; b = l * 1.02f;
+            } else {  // sun: orange granulation
+                const float n = fbm(u * 30.0f, v * 15.0f, 71u, 5);
+                r = 255.0f; g = 120.0f + 110.0f * n; b = 10.0f + 60.0f * n * n;
+            }
+            px[0] = to_u8(r);
+            px[1] = to_u8(g);
+            px[2] = to_u8(b);
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int rt_procedural_texture(int kind, int32_t width, int32_t height, uint8_t* rgb) {
+    if (kind < 0 || kind > 2 || width <= 0 || height <= 0 || !rgb) {
+        rt::set_error("rt_procedural_texture: kind must be 0..2, width and height positive, rgb non-NULL");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int32_t nthreads = (int32_t)std::max(1u, std::min(hw ? hw : 1u, 16u));
+    const int32_t chunk = (height + nthreads - 1) / nthreads;
+    std::vector<std::thread> pool;
+    pool.reserve((size_t)nthreads);
+    int32_t started_rows = 0;  // rows [0, started_rows) belong to started threads
+    for (int32_t t = 0; t < nthreads && started_rows < height; t++) {
+        const int32_t y0 = t * chunk, y1 = std::min(height, y0 + chunk);
+        try {
+            pool.emplace_back(texture_rows, kind, width, height, rgb, y0, y1);
+        } catch (const std::exception&) {  // no more threads: the rest on this one
+            break;
+        }
+        started_rows = y1;
+    }
+    if (started_rows < height) texture_rows(kind, width, height, rgb, started_rows, height);
+    for (auto& th : pool) th.join();
+    return RT_OK;
+}
 
 extern "C" int rt_builtin_scene(int which, uint32_t seed, rt_hittable_desc* hittables, uint32_t* num_hittables,
                                 rt_material_desc* materials, uint32_t* num_materials) {

@@ -325,7 +325,7 @@ __device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, 
     if (tex_type == RT_IMAGE) {
         const int img = __float_as_int(m0.w);
         if (img < 0) return mk(0.0f, 1.0f, 1.0f);  // no image (Texture.cuh:83-84: data == nullptr → cyan)
-        const int4 im = imgs[img];
+        const int4 im = imgs[img];  // (byte offset of the texels, width, height, bytes per texel)
         if (im.x < 0) return mk(0.0f, 1.0f, 1.0f);  // data == nullptr
         u = clampf(u, 0.0f, 1.0f);
         v = 1.0f - clampf(v, 0.0f, 1.0f);
@@ -334,8 +334,20 @@ __device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, 
         if (i >= im.y) i = im.y - 1;
         if (j >= im.z) j = im.z - 1;
         const float color_scale = 1.0f / 255.0f;
-        const uint8_t* px = texels + im.x + (size_t)j * (size_t)(3 * im.y) + (size_t)i * 3;
-        return mk(color_scale * (float)px[0], color_scale * (float)px[1], color_scale * (float)px[2]);
+        const size_t texel = (size_t)j * (size_t)im.y + (size_t)i;
+        uint32_t r, g, b;
+        if (im.w == 4) {  // RGBA8-padded layout: one dword gather per texel
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(texels + im.x + texel * 4);
+            r = w & 0xffu;
+            g = (w >> 8) & 0xffu;
+            b = (w >> 16) & 0xffu;
+        } else {  // the reference's RGB8 layout (Texture.cuh:76, 96-104): three byte gathers
+            const uint8_t* px = texels + im.x + texel * 3;
+            r = px[0];
+            g = px[1];
+            b = px[2];
+        }
+        return mk(color_scale * (float)r, color_scale * (float)g, color_scale * (float)b);
     }
     return mk(0.0f, 0.0f, 0.0f);
 }
@@ -1841,6 +1853,15 @@ int rt_set_tuning(int key, int value) {
         }
         int prev = g_adaptive_order;
         g_adaptive_order = value;
+        return prev;
+    }
+    if (key == RT_TUNE_TEXEL_LAYOUT) {
+        if (value != 3 && value != 4) {
+            set_error("rt_set_tuning: texel layout must be 3 (RGB8) or 4 (RGBA8)");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_texel_bytes;
+        g_texel_bytes = value;
         return prev;
     }
     if (key == RT_TUNE_LDS_PAD) {

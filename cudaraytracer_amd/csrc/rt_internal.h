@@ -18,7 +18,9 @@
 //               m0 = (bits(type | textype << 4), fuzz|ir, float(light_intensity), bits(image))
 //               m1 = (color.rgb, 0)   m2 = (color2.rgb, 0)
 //               dielectric: m1 = (1.0f / ir, r0², 0, 0) — the ir-only terms of Scatter, same binary32 ops
-//   images  : RGB8 texels of every image back to back; imgs[i] = (offset, width, height, 0) as int4
+//   images  : texels of every image back to back, RGB8 (3 B, the reference's layout, Texture.cuh:76) or
+//             RGBA8 (4 B, alpha 0: one dword gather per lookup); imgs[i] = (byte offset, width, height,
+//             bytes per texel) as int4, offset -1 = no data
 //
 // Box padding: child boxes are the reference's primitive boxes (Hittable.cuh:112-116, 171-181, ...)
 // grown outward by a relative epsilon, so the fused-multiply-add slab test of the kernel can never
@@ -37,6 +39,7 @@ namespace rt {
 constexpr int kLeafMax = 4;         // max primitives per leaf (2-bit count in the leaf reference)
 extern thread_local int g_leaf_max;  // rt_set_tuning(RT_TUNE_LEAF_MAX): 1..kLeafMax, read by the BVH build
 extern thread_local int g_sah_traversal_x10;  // rt_set_tuning(RT_TUNE_SAH_TRAVERSAL): SAH node cost × 10
+extern thread_local int g_texel_bytes;  // rt_set_tuning(RT_TUNE_TEXEL_LAYOUT): device bytes per texel, 3 or 4
 constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) traversal stack
 
 struct HostScene {

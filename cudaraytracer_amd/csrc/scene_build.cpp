@@ -183,6 +183,7 @@ int check_texture(const rt_texture_desc& t, uint32_t num_images, std::string* er
 
 thread_local int g_leaf_max = kLeafMax;
 thread_local int g_sah_traversal_x10 = 12;
+thread_local int g_texel_bytes = 3;
 
 int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images, std::vector<float>* out,
                    std::string* err) {
@@ -254,7 +255,8 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
             *err = "image " + std::to_string(i) + ": more than 2^31 texels";
             return RT_ERR_INVALID_SCENE;
         }
-        const size_t bytes = im.data ? (size_t)texels * 3 : 0;
+        const int bpt = g_texel_bytes == 4 ? 4 : 3;
+        const size_t bytes = im.data ? (size_t)texels * (size_t)bpt : 0;
         if (bytes && off + bytes > (size_t)INT32_MAX) {  // imgs[] holds 32-bit byte offsets
             *err = "images exceed 2 GiB of texels in one scene";
             return RT_ERR_INVALID_SCENE;
@@ -262,9 +264,20 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         out->imgs.push_back(bytes ? (int32_t)off : -1);
         out->imgs.push_back(im.width);
         out->imgs.push_back(im.height);
-        out->imgs.push_back(0);
+        out->imgs.push_back(bpt);
         if (bytes) {
-            out->texels.insert(out->texels.end(), im.data, im.data + bytes);
+            out->texels.resize(off + bytes);
+            uint8_t* dst = out->texels.data() + off;
+            if (bpt == 3) {
+                std::memcpy(dst, im.data, bytes);
+            } else {
+                for (size_t t = 0; t < (size_t)texels; t++) {
+                    dst[4 * t + 0] = im.data[3 * t + 0];
+                    dst[4 * t + 1] = im.data[3 * t + 1];
+                    dst[4 * t + 2] = im.data[3 * t + 2];
+                    dst[4 * t + 3] = 0;
+                }
+            }
             off += bytes;
             off = (off + 15) & ~(size_t)15;
             out->texels.resize(off, 0);

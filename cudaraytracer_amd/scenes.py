@@ -68,30 +68,31 @@ class Scene:
         return cls(h, m, list(images or []))
 
 
-def procedural_texture(width: int = 512, height: int = 256) -> np.ndarray:
-    """Deterministic RGB8 'planet' texture standing in for assets/textures/8k_*.jpg (no JPEG decoder here)."""
-    v, u = np.meshgrid(np.linspace(0.0, 1.0, height, dtype=np.float64),
-                       np.linspace(0.0, 1.0, width, dtype=np.float64), indexing="ij")
-    lat = (v - 0.5) * np.pi
-    lon = u * 2.0 * np.pi
-    land = (np.sin(3.0 * lon) * np.cos(2.0 * lat) + 0.5 * np.sin(7.0 * lon + 1.3) * np.sin(5.0 * lat)) > 0.15
-    ice = np.abs(lat) > 1.25
-    r = np.where(ice, 235, np.where(land, 70 + 60 * np.cos(lat), 20))
-    g = np.where(ice, 240, np.where(land, 120 + 40 * np.sin(lon), 60))
-    b = np.where(ice, 250, np.where(land, 40, 150 + 60 * np.cos(lat)))
-    img = np.stack([r, g, b], axis=-1)
-    return np.clip(img, 0, 255).astype(np.uint8)
+TEXTURE_EARTH, TEXTURE_MOON, TEXTURE_SUN = 0, 1, 2
+DEFAULT_TEXTURE_SIZE = (1024, 512)  # parity fixtures; BASELINE config 5 uses the reference's 8192x4096
 
 
-def builtin(which: int, seed: int = 1) -> Scene:
-    """Built-in scene `which` (see rt_builtin_scene in include/rt_hip.h)."""
+def procedural_texture(kind: int = TEXTURE_EARTH, width: int = 1024, height: int = 512) -> np.ndarray:
+    """Deterministic RGB8 (H, W, 3) stand-in for the reference's 8K planet maps (assets/textures/8k_*.jpg;
+    there is no JPEG decoder here): rt_procedural_texture in librt_hip.so (host code, no device needed)."""
+    img = np.empty((height, width, 3), dtype=np.uint8)
+    check(lib().rt_procedural_texture(kind, width, height, img.ctypes.data), "rt_procedural_texture")
+    return img
+
+
+def builtin(which: int, seed: int = 1, texture_size: tuple = DEFAULT_TEXTURE_SIZE) -> Scene:
+    """Built-in scene `which` (see rt_builtin_scene in include/rt_hip.h).  The textured scene gets three
+    procedural images (earth, moon, sun) of texture_size = (width, height)."""
     L = lib()
     nh, nm = C.c_uint32(0), C.c_uint32(0)
     check(L.rt_builtin_scene(which, seed, None, C.byref(nh), None, C.byref(nm)), "rt_builtin_scene(size)")
     h = (abi.HittableDesc * nh.value)()
     m = (abi.MaterialDesc * nm.value)()
     check(L.rt_builtin_scene(which, seed, h, C.byref(nh), m, C.byref(nm)), "rt_builtin_scene")
-    images = [procedural_texture()] if which == SCENE_TEXTURED else []
+    images = []
+    if which == SCENE_TEXTURED:
+        w, hh = texture_size
+        images = [procedural_texture(k, w, hh) for k in (TEXTURE_EARTH, TEXTURE_MOON, TEXTURE_SUN)]
     return Scene(h, m, images)
 
 
@@ -125,9 +126,14 @@ class Config:
     bg_start: tuple = DEFAULT_BG_START
     bg_end: tuple = DEFAULT_BG_END
     description: str = ""
+    texture_size: tuple = DEFAULT_TEXTURE_SIZE  # (width, height) of the textured scene's images
 
     def inputs(self) -> abi.InputStruct:
         return camera_inputs(self.position, self.orientation, self.fov, bg_start=self.bg_start, bg_end=self.bg_end)
+
+    def scene_desc(self) -> Scene:
+        """The configuration's scene, with its textures at the configured size."""
+        return builtin(self.scene, texture_size=self.texture_size)
 
     def scaled(self, width: int, height: int, spp: int | None = None) -> "Config":
         c = Config(**{k: getattr(self, k) for k in self.__dataclass_fields__})
@@ -152,7 +158,8 @@ CONFIGS = {
     "c4": Config("c4", SCENE_RTIOW, 7680, 4320, 128, 8, (13.0, 2.0, 3.0), _RTIOW_FWD, 20.0,
                  description="8 GPUs, 7680x4320, 128 spp, depth 8, RTIOW (image-tile split + gather)"),
     "c5": Config("c5", SCENE_TEXTURED, 1920, 1080, 1, 4, (0.0, 2.0, 10.0), _TEX_FWD, 45.0,
-                 description="1920x1080, 1 spp progressive, depth 4, textured spheres + moving camera"),
+                 description="1920x1080, 1 spp progressive, depth 4, textured spheres + moving camera",
+                 texture_size=(8192, 4096)),
     "default": Config("default", SCENE_DEFAULT_WORLD, 800, 600, 36, 12, (0.0, 2.0, 12.0), (0.0, 0.0, -1.0), 45.0,
                       description="the reference viewer's startup state (CudaLayer.h:66-67, 123-124)"),
 }

@@ -267,8 +267,11 @@ int rt_set_wave_trace(void* buffer);
  * order (NULL = row-major).  Results do not depend on it (every pixel is independent); the time does. */
 int rt_set_tile_order(const void* order);
 
-/* Tuning/benchmark knob (per thread): -1 = automatic; 0..5 = (scene tables staged in LDS) * 3 + traversal
- * stack kind (0 = scratch, 1 = LDS, 2 = 4 VGPRs + scratch).  Returns the previous value. */
+/* Tuning/benchmark knob (per thread): the kernel rt_render launches.  -1 = automatic (3 for spp >= 32, else 4,
+ * with fallbacks where a kernel's limits are exceeded); 0 = v1 (scratch stack, any scene), 1 = v2 (resumable,
+ * 32-bit LDS stacks), 2 = v3 (resumable, path state parked in LDS, 16-bit stacks, longest-first tile order),
+ * 3 = v3 with compact parking, 4 = v4 (v3 made persistent with a pixel work queue).  Returns the previous
+ * value. */
 int rt_set_variant(int variant);
 
 /* Tuning knob (per thread); returns the previous value or a negative rt_status.
@@ -283,8 +286,12 @@ int rt_set_variant(int variant);
  *   RT_TUNE_ADAPTIVE_ORDER: 1 (default) = the v3 kernels dispatch a frame's tiles longest-first, ordered by
  *   the per-tile wave lifetimes the previous launch on the same stream with the same tile grid measured;
  *   0 = row-major.  The image does not depend on it. */
+/*   RT_TUNE_TEXEL_LAYOUT: device bytes per texel of the images of later rt_scene_create calls: 3 (default,
+ *   the reference's RGB8 layout, Texture.cuh:76: three byte gathers per lookup) or 4 (RGBA8-padded: one dword
+ *   gather per lookup, 4/3 the memory).  The image does not depend on it. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
-                     RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5 };
+                     RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
+                     RT_TUNE_TEXEL_LAYOUT = 6 };
 int rt_set_tuning(int key, int value);
 
 /* Host-side helpers (no device needed). */
@@ -314,10 +321,15 @@ int32_t rt_glibc_rand_next(rt_glibc_rand* g);
  *   1 = 3-sphere Lambertian scene (BASELINE config 1)
  *   2 = RTIOW book-1 final random-spheres scene in the reference's types (BASELINE config 2/4)
  *   3 = Cornell-style emissive box of XY/XZ/YZ rects (BASELINE config 3)
- *   4 = textured spheres (BASELINE config 5); image 0 is a procedural RGB8 texture
+ *   4 = textured spheres (BASELINE config 5); images 0, 1, 2 (earth, moon, sun) are the caller's
  * `seed` seeds rt_glibc_srand for the scenes that draw random numbers (glibc default is 1). */
 int rt_builtin_scene(int which, uint32_t seed, rt_hittable_desc* hittables, uint32_t* num_hittables,
                      rt_material_desc* materials, uint32_t* num_materials);
+
+/* Procedural RGB8 texture (3 bytes per texel, row-major, row 0 = top as stb loads it) standing in for the
+ * reference's 8192×4096 planet maps (assets/textures/8k_*.jpg, loaded by RawStbImage.h:11-22): kind 0 = earth,
+ * 1 = moon, 2 = sun.  Deterministic: every texel is a pure function of (kind, x, y, width, height). */
+int rt_procedural_texture(int kind, int32_t width, int32_t height, uint8_t* rgb);
 
 /* Camera → InputStruct exactly as CudaLayer.cpp:43-65: up = normalize(cross(o, normalize(cross(o, up0)))). */
 void rt_camera_inputs(const float position[3], const float orientation[3], const float world_up[3],

@@ -52,7 +52,7 @@ def lib() -> C.CDLL:
         L.orc_scene_depth.argtypes = [vp]
         L.orc_scene_set_exact.argtypes = [vp, C.c_int]
         L.orc_render_init.argtypes = [vp, C.c_uint, C.c_uint, C.c_ulonglong, C.c_int]
-        L.orc_render.argtypes = [vp, vp, vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint, vp, C.POINTER(abi.InputStruct),
+        L.orc_render.argtypes = [vp, vp, vp, vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint, vp, C.POINTER(abi.InputStruct),
                                  C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_int, C.c_ulonglong,
                                  C.c_uint, C.POINTER(Counters)]
         L.orc_philox4x32_10.argtypes = [C.POINTER(C.c_uint), C.POINTER(C.c_uint), C.POINTER(C.c_uint)]
@@ -99,15 +99,19 @@ def init_states(width: int, height: int, seed_base: int = 1984, full: bool = Tru
 def render(oscene: OracleScene, width: int, height: int, spp: int, depth: int, inputs: abi.InputStruct,
            states: np.ndarray, faithful_grid: bool = False, rows: tuple | None = None, threads: int = 0,
            rius_order: int = 1, radiance: bool = False, row_step: int = 1, philox: bool = False,
-           seed: int = 1984, frame: int = 0):
+           seed: int = 1984, frame: int = 0, accum: np.ndarray | None = None):
     """One frame; returns (pos (H, W) uint32, radiance (H, W, 4) or None, Counters).  `states` advances
     (XORWOW mode); with philox=True the pixels draw from their (seed, pixel, frame) Philox streams and
-    `states` may be None."""
+    `states` may be None.  `accum` (H·W·4 float32, updated in place): progressive accumulation
+    (RT_FLAG_ACCUMULATE semantics)."""
+    if accum is not None:
+        assert accum.dtype == np.float32 and accum.size == width * height * 4 and accum.flags.c_contiguous
     pos = np.zeros(width * height, dtype=np.uint32)
     rad = np.zeros(width * height * 4, dtype=np.float32) if radiance else None
     cnt = Counters()
     r0, r1 = rows if rows else (0, height)
-    lib().orc_render(oscene.handle, pos.ctypes.data, rad.ctypes.data if rad is not None else None, width, height,
+    lib().orc_render(oscene.handle, pos.ctypes.data, rad.ctypes.data if rad is not None else None,
+                     accum.ctypes.data if accum is not None else None, width, height,
                      spp, depth, states.ctypes.data if states is not None else None, C.byref(inputs),
                      1 if faithful_grid else 0, r0, r1, row_step, threads, rius_order, 1 if philox else 0, seed, frame,
                      C.byref(cnt))

@@ -620,7 +620,7 @@ void orc_render_init(rt_curand_state* state, unsigned width, unsigned height, un
 }
 
 /* Kernel (Kernel.cu:102-158) */
-void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, unsigned width, unsigned height,
+void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, float* accum, unsigned width, unsigned height,
                 unsigned spp, unsigned max_depth, rt_curand_state* state, const rt_input_struct* in,
                 int faithful_grid, unsigned row_begin, unsigned row_end, unsigned row_step, int threads,
                 int order, int philox, unsigned long long seed, unsigned frame, orc_counters* counters) {
@@ -667,7 +667,14 @@ void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, unsigned
                 col = add(col, color(s, start, dir, (int)max_depth, &g, in, order, &c));
             }
             if (!philox) state[pixel_index] = st;
-            col = divs(col, (float)spp);
+            if (accum) { /* progressive accumulation (not in the reference): running sum of
+                            samples and sample count per pixel, the image shows their quotient */
+                float* ap = accum + 4 * (size_t)pixel_index;
+                ap[0] = ap[0] + col.x; ap[1] = ap[1] + col.y; ap[2] = ap[2] + col.z; ap[3] = ap[3] + (float)spp;
+                col = divs(mk(ap[0], ap[1], ap[2]), ap[3]);
+            } else {
+                col = divs(col, (float)spp);
+            }
             if (radiance) {
                 float* rp = radiance + 4 * (size_t)pixel_index;
                 rp[0] = col.x; rp[1] = col.y; rp[2] = col.z; rp[3] = 1.0f;

@@ -52,14 +52,16 @@ typedef struct orc_counters {
 } orc_counters;
 
 /* One frame of Kernel (Kernel.cu:102-158).  pos: W·H uint32 (row 0 = bottom); radiance: optional W·H·4
- * floats (col/spp, pre-gamma).  Only rows row_begin, row_begin + row_step, ... < row_end are rendered
+ * floats (col/spp, pre-gamma); accum: optional W·H·4 float running sum (rgb += Σ samples, w += spp; the
+ * image then shows rgb / w — the renderer's RT_FLAG_ACCUMULATE, not a reference feature).  Only rows row_begin, row_begin + row_step, ... < row_end are rendered
  * (bounded CPU-baseline samples; row_step 0 = 1).
  * faithful_grid: skip pixels outside whole 16×16 blocks (Kernel.cu:184).  threads: OpenMP threads (0 =
  * default).  rius_order: 0 = left-to-right evaluation of Vec3(ξ,ξ,ξ) in Random() (Math.cuh:231-234),
  * 1 = right-to-left (what g++ emits for that constructor call).  philox != 0: every pixel draws from the
  * Philox stream (seed, global pixel index, frame) instead of its XORWOW state; `state` is not used and may
  * be NULL. */
-void orc_render(const orc_scene* scene, unsigned int* pos, float* radiance, unsigned width, unsigned height,
+void orc_render(const orc_scene* scene, unsigned int* pos, float* radiance, float* accum, unsigned width,
+                unsigned height,
                 unsigned spp, unsigned max_depth, rt_curand_state* state, const rt_input_struct* inputs,
                 int faithful_grid, unsigned row_begin, unsigned row_end, unsigned row_step, int threads,
                 int rius_order, int philox, unsigned long long seed, unsigned frame, orc_counters* counters);

@@ -70,8 +70,8 @@ def main() -> None:
             state_after_sha256=np.frombuffer(digest(st[:, :6]), np.uint8),
             radiance_sha256=np.frombuffer(digest(rad), np.uint8),
             counters=np.array([cnt.rays, cnt.box_tests, cnt.prim_tests, cnt.primary], np.uint64),
-            texture_sha256=np.frombuffer(digest(np.asarray(sc.images[0]) if sc.images else np.zeros(0, np.uint8)),
-                                         np.uint8))
+            texture_sha256=np.frombuffer(digest(np.concatenate([np.asarray(i).ravel() for i in sc.images])
+                                                if sc.images else np.zeros(0, np.uint8)), np.uint8))
         print(case.name, pos.shape, cnt.rays, flush=True)
     for case, frame in PHILOX_CASES:
         cfg = case.cfg()

@@ -180,8 +180,8 @@ def test_reference_graph_flattens_to_the_same_scene(which):
     got = []
     for x in h:
         mm = m[x.material]
-        if mm.albedo.type == abi.RT_IMAGE:
-            mm.albedo.image = 0  # one image per textured material in the graph
+        if mm.albedo.type == abi.RT_IMAGE:  # one image per textured material in the graph: map it back
+            mm.albedo.image = [np.asarray(i).ctypes.data for i in s.images].index(im[mm.albedo.image].data)
         got.append((bytes(x.center), x.type, x.radius, x.width, x.height, bytes(mm)))
     assert sorted(got) == want
 

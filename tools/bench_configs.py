@@ -4,8 +4,9 @@ c3: 3840x2160, 256 spp, depth 16, Cornell box (one frame).
 c4: 7680x4320, 128 spp, depth 8, RTIOW: the share of rank 0 of 8 (block-cyclic 16-row bands, 270 of the
     4320 rows), i.e. the work one GPU of the 8-GPU configuration renders per frame; the gather is not
     included (one RCCL gather of 16.6 MB per rank).
-c5: 1920x1080, 1 spp, depth 4, textured spheres, progressive accumulation with the scripted moving camera
-    (accumulation resets when the camera moves; here every frame moves, as in an interactive orbit).
+c5: 1920x1080, 1 spp, depth 4, textured spheres with three 8192x4096 textures (RGB8, or RGBA8-padded with
+    --texel-layouts 4), progressive accumulation with the scripted moving camera (accumulation resets when the
+    camera moves; here every frame moves, as in an interactive orbit).
 Each config runs with the reference's XORWOW state (parity mode) and with the stateless Philox streams.
 """
 import argparse, json, os, sys
@@ -19,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--variants", default="-1", help="kernel variants to time (rt_set_variant), comma-separated")
 ap.add_argument("--configs", default="c3,c4,c5")
 ap.add_argument("--rngs", default="xorwow,philox")
+ap.add_argument("--texel-layouts", default="3,4", help="c5: device bytes per texel (RT_TUNE_TEXEL_LAYOUT)")
 args = ap.parse_args()
 
 
@@ -31,12 +33,27 @@ def timed(fn):
     return e0.elapsed_time(e1)
 
 
-def run(variant, config, rng):
+_scenes = {}
+
+
+def scene_for(config, layout):
+    key = (config, layout)
+    if key not in _scenes:
+        prev = lib().rt_set_tuning(6, layout)
+        _scenes[key] = DeviceScene(scenes.CONFIGS[config].scene_desc())
+        lib().rt_set_tuning(6, prev)
+    return _scenes[key]
+
+
+def run(variant, config, rng, layout=3):
     lib().rt_set_variant(variant)
     cfg = scenes.CONFIGS[config]
-    ds = DeviceScene(scenes.builtin(cfg.scene))
+    ds = scene_for(config, layout)
     out = {"config": config, "rng": rng, "variant": variant,
            "workload": f"{cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}"}
+    if config == "c5":
+        out["texel_bytes"] = layout
+        out["texture_size"] = list(cfg.texture_size)
     if config == "c5":
         r = Renderer(cfg.width, cfg.height, rng=rng)
         r.render_init()
@@ -69,4 +86,5 @@ def run(variant, config, rng):
 for v in (int(x) for x in args.variants.split(",")):
     for config in args.configs.split(","):
         for rng in args.rngs.split(","):
-            print(json.dumps(run(v, config, rng)), flush=True)
+            for layout in ([int(x) for x in args.texel_layouts.split(",")] if config == "c5" else [3]):
+                print(json.dumps(run(v, config, rng, layout)), flush=True)

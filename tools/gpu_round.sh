@@ -1,13 +1,31 @@
 #!/bin/bash
-# One GPU session: parity tests, bench, rocprofv3 kernel-trace summary.  Stops at the first GPU fault,
-# abort, segfault or timeout (pytest rc 1 = test failures only, which does not stop the session).
+# One GPU session (run through gpurun from the repo root): parity tests, smoke, bench + rocprofv3 kernel
+# summary, per-config timings.  Every GPU step has its own time limit and the session stops at the first
+# GPU fault, abort, segfault or timeout (pytest rc 1 = test failures only, which does not stop it).
+#   STEPS="tests smoke bench prof configs"   (default: all)   PYTEST_ARGS=...   BENCH_ARGS=...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench_prof.log 2>&1 || exit $?
+STEPS=${STEPS:-tests smoke bench prof configs}
+for step in $STEPS; do
+  case $step in
+    tests)
+      timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread \
+        ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; tail -3 gpurun_out/pytest_gpu.log
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
+    smoke)
+      timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 || exit $? ;;
+    bench)
+      timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || exit $?
+      tail -1 gpurun_out/bench.log ;;
+    prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
+        python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench_prof.log 2>&1 || exit $? ;;
+    configs)
+      timeout -k 10 400 python tools/bench_configs.py ${CONFIGS_ARGS:-} > gpurun_out/configs.log 2>&1 || exit $?
+      cat gpurun_out/configs.log | grep -v amdgpu.ids ;;
+  esac
+done
 echo done
