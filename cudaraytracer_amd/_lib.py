@@ -28,10 +28,14 @@ EXPORTED = [
     "rt_scene_get_info",
     "rt_render_init",
     "rt_render",
+    "rt_tiled_create",
+    "rt_tiled_render",
+    "rt_tiled_destroy",
     "rt_set_timing",
     "rt_set_wave_trace",
     "rt_set_tile_order",
     "rt_last_kernel_ms",
+    "rt_last_launch_host_ms",
     "rt_set_variant",
     "rt_set_tuning",
     "rt_glibc_srand",
@@ -64,9 +68,13 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_render_init.argtypes = [vp, C.c_uint32, C.c_uint32, P(abi.Tiling), C.c_uint64, vp]
     lib.rt_render.argtypes = [vp, P(abi.RenderArgs), vp]
     lib.rt_set_timing.argtypes = [C.c_int]
+    lib.rt_tiled_create.argtypes = [P(abi.TiledDesc), P(abi.SceneDesc), P(vp)]
+    lib.rt_tiled_render.argtypes = [vp, P(abi.TiledFrame), P(abi.TiledTiming)]
+    lib.rt_tiled_destroy.argtypes = [vp]
     lib.rt_set_wave_trace.argtypes = [C.c_void_p]
     lib.rt_set_tile_order.argtypes = [C.c_void_p]
     lib.rt_last_kernel_ms.restype = C.c_float
+    lib.rt_last_launch_host_ms.restype = C.c_float
     lib.rt_set_variant.argtypes = [C.c_int]
     lib.rt_set_tuning.argtypes = [C.c_int, C.c_int]
     lib.rt_glibc_srand.argtypes = [P(abi.GlibcRand), C.c_uint32]

@@ -139,6 +139,23 @@ class RenderArgs(C.Structure):
     ]
 
 
+class TiledDesc(C.Structure):
+    _fields_ = [("devices", C.POINTER(C.c_int)), ("num_ranks", C.c_uint32), ("band_rows", C.c_uint32),
+                ("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32),
+                ("seed", C.c_uint64)]
+
+
+class TiledFrame(C.Structure):
+    _fields_ = [("pos", C.c_void_p), ("samples_per_pixel", C.c_uint32), ("max_depth", C.c_uint32),
+                ("flags", C.c_uint32), ("rng_frame", C.c_uint32), ("rng_frame_set", C.c_uint32),
+                ("reserved", C.c_uint32), ("inputs", InputStruct)]
+
+
+class TiledTiming(C.Structure):
+    _fields_ = [("render_ms", C.c_float), ("gather_ms", C.c_float), ("total_ms", C.c_float), ("reserved", C.c_uint32),
+                ("rays", C.c_uint64)]
+
+
 class SceneInfo(C.Structure):
     _fields_ = [
         ("num_primitives", C.c_uint32),

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <stdexcept>
 #include <cstring>
@@ -46,7 +47,11 @@ static int upload(const std::vector<T>& host, void** dev, const char* what) {
     hipError_t e = hipMalloc(dev, host.size() * sizeof(T));
     if (e != hipSuccess) return hip_fail(e, what);
     e = hipMemcpy(*dev, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e, what);
+    if (e != hipSuccess) {
+        (void)hipFree(*dev);
+        *dev = nullptr;
+        return hip_fail(e, what);
+    }
     return RT_OK;
 }
 
@@ -57,16 +62,16 @@ static void free_device(DeviceScene* s) {
     s->nodes48 = s->refs16 = nullptr;
     if (s->prims) (void)hipFree((void*)s->prims);
     if (s->mats) (void)hipFree((void*)s->mats);
-    if (s->imgs) (void)hipFree((void*)s->imgs);
-    if (s->texels) (void)hipFree((void*)s->texels);
+    if (s->imgs) (void)hipFree((void*)s->imgs);  // texels: owned by rt_scene::texel_block
     s->nodes = s->prims = s->mats = nullptr;
     s->imgs = nullptr;
     s->texels = nullptr;
 }
 
-int create_device_scene(const HostScene& h, rt_scene** out) {
+int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void> shared_texels) {
     rt_scene* s = new rt_scene();
     s->host = h;
+    s->host.texels = std::vector<uint8_t>();  // uploaded below (or shared); no host copy is kept
     DeviceScene& d = s->dev;
     int rc;
     void* p;
@@ -82,15 +87,21 @@ int create_device_scene(const HostScene& h, rt_scene** out) {
     d.mats = p;
     if ((rc = upload(h.imgs, &p, "hipMalloc/hipMemcpy(images)"))) goto fail;
     d.imgs = p;
-    if ((rc = upload(h.texels, &p, "hipMalloc/hipMemcpy(texels)"))) goto fail;
-    d.texels = p;
+    if (shared_texels) {
+        s->texel_block = std::move(shared_texels);
+    } else {
+        if ((rc = upload(h.texels, &p, "hipMalloc/hipMemcpy(texels)"))) goto fail;
+        if (p) s->texel_block = std::shared_ptr<void>(p, [](void* q) { (void)hipFree(q); });
+    }
+    d.texels = s->texel_block.get();
     d.num_nodes = h.num_nodes;
     d.num_prims = h.num_prims;
     d.num_mats = h.num_mats;
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;
-    d.device_bytes = (h.nodes.size() + h.prims.size() + h.mats.size()) * 4 + h.imgs.size() * 4 + h.texels.size();
+    d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs16.size() + h.prims.size() + h.mats.size()) * 4 +
+                     h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;
 fail:
@@ -213,6 +224,107 @@ int flatten_reference_graph(const void* world, FlatDesc* out, std::string* err) 
         out->hittables.push_back(d);
     }
     return RT_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// LaunchKernel's scene cache.  The viewer mutates its managed-memory graph in place
+// between frames without notifying anyone, so every launch re-flattens it (microseconds for ~500
+// objects) and compares the flat description with the cached one:
+//   * hittables (geometry, activity) differ → rebuild BVH + tables, keep the uploaded texels;
+//   * only materials differ → re-upload the material table in place (no rebuild, CudaLayer.cpp:719-872);
+//   * an image's (data pointer, width, height) differs → rebuild with a new texel upload.  The reference
+//     replaces texture data by cudaFree + a new allocation (CudaLayer.cpp:889-903), so the pointer is the
+//     change key: texel bytes are never read per frame.
+// One entry per (device, world pointer), least recently used evicted beyond kLaunchCacheEntries.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+struct ImageKey {
+    const void* data;
+    int32_t width, height;
+    bool operator==(const ImageKey& o) const { return data == o.data && width == o.width && height == o.height; }
+};
+
+struct LaunchEntry {
+    int device = 0;
+    const void* world = nullptr;
+    uint64_t last_use = 0;
+    std::vector<rt_hittable_desc> hittables;
+    std::vector<rt_material_desc> materials;
+    std::vector<ImageKey> images;
+    rt_scene* scene = nullptr;
+};
+
+constexpr size_t kLaunchCacheEntries = 8;
+std::mutex g_launch_mu;
+std::vector<LaunchEntry> g_launch_cache;
+uint64_t g_launch_clock = 0;
+
+template <class T>
+bool same_bytes(const std::vector<T>& a, const std::vector<T>& b) {
+    return a.size() == b.size() && (a.empty() || std::memcmp(a.data(), b.data(), a.size() * sizeof(T)) == 0);
+}
+
+}  // namespace
+
+int reference_scene_for_launch(const void* world, rt_scene** out, double* host_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int device = 0;
+    hipError_t e = hipGetDevice(&device);
+    if (e != hipSuccess) return hip_fail(e, "LaunchKernel: hipGetDevice");
+    std::lock_guard<std::mutex> lock(g_launch_mu);
+    int rc = guarded("LaunchKernel", [&]() -> int {
+        FlatDesc f;
+        std::string err;
+        int r = flatten_reference_graph(world, &f, &err);
+        if (r) { set_error("LaunchKernel: " + err); return r; }
+        std::vector<ImageKey> images;
+        for (const rt_image_desc& im : f.images) images.push_back(ImageKey{im.data, im.width, im.height});
+        LaunchEntry* ent = nullptr;
+        for (LaunchEntry& c : g_launch_cache)
+            if (c.device == device && c.world == world) ent = &c;
+        if (!ent) {
+            if (g_launch_cache.size() >= kLaunchCacheEntries) {  // evict the least recently used entry
+                auto lru = std::min_element(g_launch_cache.begin(), g_launch_cache.end(),
+                                            [](const LaunchEntry& a, const LaunchEntry& b) { return a.last_use < b.last_use; });
+                int cur = 0;
+                (void)hipGetDevice(&cur);
+                (void)hipSetDevice(lru->device);
+                rt_scene_destroy(lru->scene);
+                (void)hipSetDevice(cur);
+                g_launch_cache.erase(lru);
+            }
+            g_launch_cache.emplace_back();
+            ent = &g_launch_cache.back();
+            ent->device = device;
+            ent->world = world;
+        }
+        ent->last_use = ++g_launch_clock;
+        const bool geometry = !ent->scene || !same_bytes(ent->hittables, f.hittables) ||
+                              ent->materials.size() != f.materials.size();
+        const bool new_images = !ent->scene || !(ent->images == images);
+        if (geometry || new_images) {
+            rt_scene_desc d = f.desc();
+            HostScene h;
+            r = build_host_scene(&d, &h, &err, new_images);
+            if (r) { set_error("LaunchKernel: " + err); return r; }
+            rt_scene* fresh = nullptr;
+            r = create_device_scene(h, &fresh, new_images ? nullptr : ent->scene->texel_block);
+            if (r) return r;
+            rt_scene_destroy(ent->scene);
+            ent->scene = fresh;
+        } else if (!same_bytes(ent->materials, f.materials)) {
+            r = rt_scene_update_materials(ent->scene, f.materials.data(), (uint32_t)f.materials.size());
+            if (r) return r;
+        }
+        ent->hittables.swap(f.hittables);
+        ent->materials.swap(f.materials);
+        ent->images.swap(images);
+        *out = ent->scene;
+        return RT_OK;
+    });
+    if (host_ms) *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
 }
 
 }  // namespace rt

@@ -1628,6 +1628,7 @@ namespace {
 
 thread_local bool g_timing = false;
 thread_local float g_last_ms = -1.0f;
+thread_local float g_last_host_ms = -1.0f;  // LaunchKernel: host time of the scene-cache step
 thread_local int g_variant = -1;
 
 int hip_check(hipError_t e, const char* what, int code = RT_ERR_DEVICE) {
@@ -1810,6 +1811,8 @@ int rt_set_timing(int enabled) {
 }
 
 float rt_last_kernel_ms(void) { return g_last_ms; }
+
+float rt_last_launch_host_ms(void) { return g_last_host_ms; }
 
 // Benchmark/tuning knob: -1 = automatic, else an index into kVariants.  Returns the previous value.
 int rt_set_variant(int variant) {
@@ -2137,33 +2140,13 @@ void LaunchRandInit(rt_curand_state* d_rand_state2) {
 void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int image_height,
                   const unsigned int samples_per_pixel, const unsigned int max_depth, const void* world,
                   rt_curand_state* d_rand_state, rt_input_struct inputs) {
-    // The viewer mutates the graph in place between frames: re-flatten every call,
-    // re-upload only when the flattened scene changed.
-    static std::mutex mu;
-    static std::vector<uint8_t> last_key;
-    static rt_scene* cached = nullptr;
-    std::lock_guard<std::mutex> lock(mu);
-    FlatDesc f;
-    std::string err;
-    if (flatten_reference_graph(world, &f, &err) != RT_OK) {
-        set_error("LaunchKernel: " + err);
-        return;
-    }
-    std::vector<uint8_t> key;
-    auto append = [&](const void* p, size_t n) { key.insert(key.end(), (const uint8_t*)p, (const uint8_t*)p + n); };
-    append(f.hittables.data(), f.hittables.size() * sizeof(rt_hittable_desc));
-    append(f.materials.data(), f.materials.size() * sizeof(rt_material_desc));
-    for (const rt_image_desc& im : f.images) {
-        append(&im, sizeof(im));
-        if (im.data) append(im.data, (size_t)im.width * im.height * 3);
-    }
-    if (!cached || key != last_key) {
-        rt_scene_destroy(cached);
-        cached = nullptr;
-        rt_scene_desc d = f.desc();
-        if (rt_scene_create(&d, &cached) != RT_OK) return;
-        last_key.swap(key);
-    }
+    // The viewer mutates the graph in place between frames: the cache re-flattens it on
+    // every call and updates the device scene by what changed (reference_scene_for_launch, api.cpp).
+    rt_scene* cached = nullptr;
+    double host_ms = 0.0;
+    const int rc = reference_scene_for_launch(world, &cached, &host_ms);
+    g_last_host_ms = (float)host_ms;
+    if (rc != RT_OK) return;
     rt_render_args a;
     std::memset(&a, 0, sizeof(a));
     a.pos = pos;

@@ -59,8 +59,9 @@ struct HostScene {
     std::vector<int32_t> prim_source;  // desc index of each primitive (BVH order)
 };
 
-// Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.
-int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err);
+// Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.  with_texels = false computes
+// the image table but leaves `texels` empty (a rebuild that reuses an uploaded texel block).
+int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, bool with_texels = true);
 
 // Material table packing only (used by rt_scene_update_materials).
 int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images, std::vector<float>* out,

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 
 #include "rt_internal.h"
 
@@ -21,11 +22,20 @@ struct DeviceScene {
     uint64_t device_bytes = 0;
 };
 
-int create_device_scene(const HostScene& h, rt_scene** out);
+// Upload the tables of `h` to the current device.  shared_texels: an existing device texel block (same image
+// table) to reference instead of uploading h.texels.  The host copy of the texels is not kept.
+int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void> shared_texels = nullptr);
+
+// The device scene of the reference graph `world` for LaunchKernel (Kernel.cu:178-191), cached per
+// (device, world): materials edited in place are re-uploaded, geometry edits rebuild the BVH and tables but
+// keep the uploaded texels, a new image (data pointer, width or height, CudaLayer.cpp:889-903) re-uploads
+// them.  *host_ms: host time spent (flatten + compare + any update).
+int reference_scene_for_launch(const void* world, rt_scene** out, double* host_ms);
 
 }  // namespace rt
 
 struct rt_scene {
-    rt::HostScene host;
+    rt::HostScene host;  // packed tables (texels dropped after the upload)
     rt::DeviceScene dev;
+    std::shared_ptr<void> texel_block;  // device texels, shared by scenes rebuilt from the same images
 };

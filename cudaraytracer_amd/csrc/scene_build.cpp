@@ -224,7 +224,7 @@ int pack_materials(const rt_material_desc* mats, uint32_t n, uint32_t num_images
     return RT_OK;
 }
 
-int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err) {
+int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, bool with_texels) {
     if (!desc) { *err = "scene description is NULL"; return RT_ERR_INVALID_ARGUMENT; }
     if ((desc->num_hittables && !desc->hittables) || (desc->num_materials && !desc->materials) ||
         (desc->num_images && !desc->images)) {
@@ -265,7 +265,9 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         out->imgs.push_back(im.width);
         out->imgs.push_back(im.height);
         out->imgs.push_back(bpt);
-        if (bytes) {
+        if (bytes && !with_texels) {
+            off = (off + bytes + 15) & ~(size_t)15;
+        } else if (bytes) {
             out->texels.resize(off + bytes);
             uint8_t* dst = out->texels.data() + off;
             if (bpt == 3) {

@@ -152,3 +152,46 @@ class Renderer:
 
     def radiance_image(self) -> np.ndarray:
         return self.radiance.cpu().numpy().reshape(self.local_rows, self.width, 4)
+
+
+class TiledRenderer:
+    """Single-process multi-device tiling through librt_hip.so (rt_tiled_*): rank r renders the block-cyclic
+    row bands b ≡ r (mod N) on devices[r] and copies them into their rows of the gathered frame (one strided
+    peer copy per rank).  The C-ABI path a C++ viewer uses for the north star's 8-GPU split, without torch."""
+
+    def __init__(self, width: int, height: int, devices, scene: Scene, band_rows: int = 16, rng: str = "xorwow",
+                 seed: int = 1984):
+        if not torch.cuda.is_available():
+            raise RTError("no HIP device visible: librt_hip.so renders on MI355X only")
+        self.width, self.height = width, height
+        self.devices = list(devices)
+        self._devs = (C.c_int * len(self.devices))(*self.devices)
+        d = abi.TiledDesc(C.cast(self._devs, C.POINTER(C.c_int)), len(self.devices), band_rows, width, height,
+                          abi.RT_FLAG_RNG_PHILOX if rng == "philox" else 0, 0, seed)
+        self._scene_desc = scene.desc()
+        self.handle = C.c_void_p()
+        check(lib().rt_tiled_create(C.byref(d), C.byref(self._scene_desc), C.byref(self.handle)), "rt_tiled_create")
+        self.pos = torch.zeros(width * height, dtype=torch.int32, device=torch.device("cuda", self.devices[0]))
+        self.timing = abi.TiledTiming()
+
+    def render(self, spp: int, max_depth: int, inputs: abi.InputStruct, flags: int = 0, frame: int | None = None,
+               pos: torch.Tensor | None = None) -> torch.Tensor:
+        """One frame over all ranks, gathered into `pos` (default: a buffer on devices[0]); synchronous."""
+        out = self.pos if pos is None else pos
+        f = abi.TiledFrame(out.data_ptr(), spp, max_depth, flags, frame or 0, 0 if frame is None else 1, 0, inputs)
+        check(lib().rt_tiled_render(self.handle, C.byref(f), C.byref(self.timing)), "rt_tiled_render")
+        return out
+
+    def image(self) -> np.ndarray:
+        return self.pos.cpu().numpy().view(np.uint32).reshape(self.height, self.width)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().rt_tiled_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

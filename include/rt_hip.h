@@ -144,7 +144,10 @@ typedef void* rt_stream;          /* hipStream_t */
  * image_height, const unsigned int samples_per_pixel, const unsigned int max_depth, Hittable* world,
  * curandState* d_rand_state, InputStruct inputs)` — Kernel.cu:178-191.
  * `world` is the reference's Hittable* scene graph (see rt_reference_graph.h); it is re-flattened on
- * every call because the viewer mutates it in place.  Floor-division grid as in
+ * every call because the viewer mutates it in place and the device scene cached per
+ * (device, world) is updated by what changed: materials in place, geometry by a BVH rebuild, images only
+ * when an image's data pointer, width or height changes (the reference re-allocates texture data to change
+ * it, CudaLayer.cpp:889-903; texel bytes are never re-read per frame).  Floor-division grid as in
  * Kernel.cu:184: pixels outside the last whole 16×16 block are not written.  Errors: rt_last_error(). */
 void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int image_height,
                   const unsigned int samples_per_pixel, const unsigned int max_depth, const void* world,
@@ -259,6 +262,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* args, rt_stream strea
 int rt_set_timing(int enabled);
 float rt_last_kernel_ms(void);
 
+/* Host milliseconds of the last LaunchKernel's scene step on this thread (graph flatten + change detection +
+ * any device update); < 0 before the first call. */
+float rt_last_launch_host_ms(void);
+
 /* Diagnostic (per thread): device buffer of 2 × uint64 per wave that later v3 launches fill with each wave's
  * start and end s_memrealtime (100 MHz) — occupancy/tail analysis (tools/wave_timeline.py).  NULL = off. */
 int rt_set_wave_trace(void* buffer);
@@ -293,6 +300,52 @@ enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6 };
 int rt_set_tuning(int key, int value);
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Multi-device image tiling in one process (the reference is single-device,    */
+/* LaunchKernel at Kernel.cu:178-191).  Band rank r renders the block-cyclic row bands b ≡ r (mod N) */
+/* on devices[r] (entries may repeat a device: one stream per rank), then copies its bands into     */
+/* their rows of the caller's W·H framebuffer with one strided peer copy over xGMI: gather and      */
+/* unshuffle in one transfer per rank.  The frame is bit-identical to a one-rank render (the RNG    */
+/* streams are keyed by the global pixel index).                                                     */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct rt_tiled rt_tiled; /* opaque: per-rank device scene, stream, framebuffer band store, RNG states */
+
+typedef struct rt_tiled_desc {
+    const int* devices;  /* device ordinal of each band rank (copied) */
+    uint32_t num_ranks;
+    uint32_t band_rows;  /* rows per band (0 = 16) */
+    uint32_t width, height;
+    uint32_t flags;      /* RT_FLAG_RNG_PHILOX: stateless Philox streams, no per-rank RNG state */
+    uint32_t reserved;   /* must be 0 */
+    uint64_t seed;       /* XORWOW: curand_init(seed + global pixel index, 0, 0) (Kernel.cu:175; 1984); Philox key */
+} rt_tiled_desc;
+
+typedef struct rt_tiled_frame {
+    uint32_t* pos;       /* device W·H RGBA8 framebuffer (row 0 = bottom) on any device: the gather target */
+    uint32_t samples_per_pixel;
+    uint32_t max_depth;
+    uint32_t flags;      /* RT_FLAG_FAITHFUL_GRID / NO_STATE_WRITEBACK / COUNT_TESTS / RIUS_LEFT_TO_RIGHT */
+    uint32_t rng_frame;  /* Philox frame counter when rng_frame_set != 0, else the object's own counter */
+    uint32_t rng_frame_set;
+    uint32_t reserved;   /* must be 0 */
+    rt_input_struct inputs;
+} rt_tiled_frame;
+
+typedef struct rt_tiled_timing {
+    float render_ms;     /* slowest rank's kernel time (HIP events on its stream) */
+    float gather_ms;     /* slowest rank's gather copy (HIP events on its stream) */
+    float total_ms;      /* host wall time of the call */
+    uint32_t reserved;
+    uint64_t rays;       /* closest-hit queries over all ranks */
+} rt_tiled_timing;
+
+/* Uploads `scene` to every distinct device, allocates each rank's band store and seeds its RNG states. */
+int rt_tiled_create(const rt_tiled_desc* desc, const rt_scene_desc* scene, rt_tiled** out);
+/* One frame over all ranks + the gather into frame->pos; synchronous (as LaunchKernel, Kernel.cu:190).
+ * timing may be NULL. */
+int rt_tiled_render(rt_tiled* tiled, const rt_tiled_frame* frame, rt_tiled_timing* timing);
+int rt_tiled_destroy(rt_tiled* tiled);
 
 /* Host-side helpers (no device needed). */
 
