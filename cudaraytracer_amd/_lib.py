@@ -31,6 +31,11 @@ EXPORTED = [
     "rt_tiled_create",
     "rt_tiled_render",
     "rt_tiled_destroy",
+    "rt_gl_register_texture",
+    "rt_gl_copy_image",
+    "rt_gl_unregister",
+    "rt_copy_image_to_host",
+    "rt_write_ppm",
     "rt_set_timing",
     "rt_set_wave_trace",
     "rt_set_tile_order",
@@ -71,6 +76,11 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_tiled_create.argtypes = [P(abi.TiledDesc), P(abi.SceneDesc), P(vp)]
     lib.rt_tiled_render.argtypes = [vp, P(abi.TiledFrame), P(abi.TiledTiming)]
     lib.rt_tiled_destroy.argtypes = [vp]
+    lib.rt_gl_register_texture.argtypes = [C.c_uint32, C.c_uint32, P(vp)]
+    lib.rt_gl_copy_image.argtypes = [vp, vp, C.c_uint32, C.c_uint32, vp]
+    lib.rt_gl_unregister.argtypes = [vp]
+    lib.rt_copy_image_to_host.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_int, vp]
+    lib.rt_write_ppm.argtypes = [C.c_char_p, vp, C.c_uint32, C.c_uint32, C.c_int]
     lib.rt_set_wave_trace.argtypes = [C.c_void_p]
     lib.rt_set_tile_order.argtypes = [C.c_void_p]
     lib.rt_last_kernel_ms.restype = C.c_float

@@ -313,6 +313,41 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
     return hit;
 }
 
+// acos / atan2 of GetSphereUV (Hittable.cuh:119-125) as fixed sequences of binary32 +, -, *, / and sqrt
+// (Cephes asinf/atanf polynomials, ~2 ulp), identical operation for operation in oracle/rt_oracle.c.  The
+// reference's CUDA acos/atan2 under -use_fast_math cannot be reproduced, and the device library's and
+// libm's acosf/atan2f disagree in the last bit now and then, which moves a lookup into an 8192-wide texture
+// by one texel.  The acos argument is clamped to [-1, 1] (a rounded normal can exceed 1 by an ulp).
+__device__ __forceinline__ float rt_asin_poly(const float x) {  // |x| <= 0.5
+    const float z = x * x;
+    const float p = (((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+                    1.6666752422e-1f;
+    return p * z * x + x;
+}
+__device__ __forceinline__ float rt_acosf(float x) {
+    x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+    if (x < -0.5f) return 0x1.921fb6p+1f - 2.0f * rt_asin_poly(sqrtf(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * rt_asin_poly(sqrtf(0.5f * (1.0f - x)));
+    return 0x1.921fb6p+0f - rt_asin_poly(x);
+}
+__device__ __forceinline__ float rt_atan_poly(const float x) {  // |x| <= tan(pi/8)
+    const float z = x * x;
+    return (((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x + x;
+}
+__device__ __forceinline__ float rt_atan01(const float t) {  // t in [0, 1]
+    if (t > 0.41421356f) return 0x1.921fb6p-1f + rt_atan_poly((t - 1.0f) / (t + 1.0f));
+    return rt_atan_poly(t);
+}
+__device__ __forceinline__ float rt_atan2f(const float y, const float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    float r;
+    if (ax == 0.0f && ay == 0.0f) r = 0.0f;
+    else if (ay <= ax) r = rt_atan01(ay / ax);
+    else r = 0x1.921fb6p+0f - rt_atan01(ax / ay);
+    if (__builtin_signbit(x)) r = 0x1.921fb6p+1f - r;  // IEEE atan2: x < 0 or -0
+    return __builtin_signbit(y) ? -r : r;
+}
+
 // Texture::value (Texture.cuh:42-45, 58-67, 83-105)
 __device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, const float4& m2, uint32_t tex_type,
                                             float u, float v, f3 p, const int4* __restrict__ imgs,
@@ -418,8 +453,8 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         p = add(ro, scale(t, rd));
         normal = divs_rn(sub(p, xyz(p0)), p0.w, p1.y);  // p1.y = RN(1/radius) or 0 (scene_build.cpp)
         if (TEX && ttype == RT_IMAGE && mtype != RT_DIELECTRIC) {  // GetSphereUV (Hittable.cuh:119-125)
-            const float theta = acosf(-normal.y);
-            const float phi = atan2f(-normal.z, normal.x) + 3.141592654f;
+            const float theta = rt_acosf(-normal.y);
+            const float phi = rt_atan2f(-normal.z, normal.x) + 3.141592654f;
             hu = phi / (2 * 3.141592654f);
             hv = theta / 3.141592654f;
         }

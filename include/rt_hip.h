@@ -347,6 +347,29 @@ int rt_tiled_create(const rt_tiled_desc* desc, const rt_scene_desc* scene, rt_ti
 int rt_tiled_render(rt_tiled* tiled, const rt_tiled_frame* frame, rt_tiled_timing* timing);
 int rt_tiled_destroy(rt_tiled* tiled);
 
+/* ------------------------------------------------------------------------------------------------ */
+/* Display and headless output of the RGBA8 framebuffer.                        */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct rt_gl_target rt_gl_target; /* opaque: a registered OpenGL texture */
+
+/* Replaces cudaGraphicsGLRegisterImage(&res, texture, GL_TEXTURE_2D, cudaGraphicsRegisterFlagsWriteDiscard)
+ * (CudaLayer.cpp:89-90).  Needs the caller's current GL context; gl_target is e.g. GL_TEXTURE_2D (0x0DE1). */
+int rt_gl_register_texture(uint32_t gl_texture, uint32_t gl_target, rt_gl_target** out);
+/* Replaces the per-frame map → mapped array → cudaMemcpy2DToArray(W·4 B × H rows, device to device) → unmap
+ * (CudaLayer.cpp:379-386), on `stream`. */
+int rt_gl_copy_image(rt_gl_target* target, const uint32_t* device_pos, uint32_t width, uint32_t height,
+                     rt_stream stream);
+int rt_gl_unregister(rt_gl_target* target);
+
+/* Host-staging fallback when there is no GL interop: the device framebuffer into host memory (synchronous on
+ * `stream`); flip_rows != 0 puts the image's top row first (buffer row 0 is the bottom, CudaLayer.cpp:402). */
+int rt_copy_image_to_host(uint32_t* host, const uint32_t* device_pos, uint32_t width, uint32_t height, int flip_rows,
+                          rt_stream stream);
+
+/* Headless output: binary PPM (P6) of a host RGBA8 buffer; flip_rows != 0 writes buffer row H-1 first, so the
+ * file shows the image upright (the reference's display flip, CudaLayer.cpp:402). */
+int rt_write_ppm(const char* path, const uint32_t* rgba, uint32_t width, uint32_t height, int flip_rows);
+
 /* Host-side helpers (no device needed). */
 
 /* Flatten the reference's Hittable* graph (rt_reference_graph.h) into flat arrays (size query with NULL

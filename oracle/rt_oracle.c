@@ -210,10 +210,48 @@ static inline void set_face_normal(hitrec* rec, v3 d, v3 outward) {
     rec->normal = rec->front_face ? outward : neg(outward);
 }
 
+/* acos / atan2 of GetSphereUV as a fixed sequence of binary32 +, -, *, / and sqrtf (Cephes asinf/atanf
+   polynomials), operation for operation the same as render.hip's rt_acosf / rt_atan2f.  The reference calls
+   CUDA's acos/atan2 under -use_fast_math (CudaRayTracer/CMakeLists.txt:36), which no CPU or ROCm library
+   reproduces; libm's and the device library's own acosf/atan2f differ in the last bit now and then, which
+   moves an 8192-wide texture lookup by one texel.  Documented deviation: the acos argument is clamped to
+   [-1, 1] (a rounded normal can exceed 1 by an ulp; the reference's NaN would index the texture with
+   int(NaN), undefined). */
+static inline float orc_asin_poly(float x) { /* |x| <= 0.5 */
+    float z = x * x;
+    float p = (((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+              1.6666752422e-1f;
+    return p * z * x + x;
+}
+static inline float orc_acosf(float x) {
+    x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+    if (x < -0.5f) return 0x1.921fb6p+1f - 2.0f * orc_asin_poly(sqrtf(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * orc_asin_poly(sqrtf(0.5f * (1.0f - x)));
+    return 0x1.921fb6p+0f - orc_asin_poly(x);
+}
+static inline float orc_atan_poly(float x) { /* |x| <= tan(pi/8) */
+    float z = x * x;
+    return (((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x + x;
+}
+static inline float orc_atan01(float t) { /* t in [0, 1] */
+    if (t > 0.41421356f) return 0x1.921fb6p-1f + orc_atan_poly((t - 1.0f) / (t + 1.0f));
+    return orc_atan_poly(t);
+}
+static inline float orc_atan2f(float y, float x) {
+    float ax = fabsf(x), ay = fabsf(y), r;
+    if (ax == 0.0f && ay == 0.0f) r = 0.0f;
+    else if (ay <= ax) r = orc_atan01(ay / ax);
+    else r = 0x1.921fb6p+0f - orc_atan01(ax / ay);
+    if (signbit(x)) r = 0x1.921fb6p+1f - r; /* IEEE atan2: x < 0 or -0 */
+    return signbit(y) ? -r : r;
+}
+float orc_acos(float x) { return orc_acosf(x); }
+float orc_atan2(float y, float x) { return orc_atan2f(y, x); }
+
 /* GetSphereUV (Hittable.cuh:119-125) */
 static inline void sphere_uv(v3 p, float* u, float* v) {
-    float theta = acosf(-p.y);
-    float phi = atan2f(-p.z, p.x) + ORC_PI;
+    float theta = orc_acosf(-p.y);
+    float phi = orc_atan2f(-p.z, p.x) + ORC_PI;
     *u = phi / (2 * ORC_PI);
     *v = theta / ORC_PI;
 }

@@ -43,6 +43,10 @@ void orc_scene_set_exact(orc_scene* s, int exact);
 
 /* RenderInit (Kernel.cu:166-176) for the (floor-division) grid gx×gy of 16×16 blocks, or for every pixel
  * when full != 0. */
+/* GetSphereUV's acos / atan2 (fixed binary32 sequences shared with the kernel, see rt_oracle.c). */
+float orc_acos(float x);
+float orc_atan2(float y, float x);
+
 void orc_render_init(rt_curand_state* state, unsigned width, unsigned height, unsigned long long seed_base,
                      int full);
 

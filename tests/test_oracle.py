@@ -310,3 +310,25 @@ def test_philox_mode_estimates_the_same_image():
     _, rp1, _ = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), None, radiance=True,
                           philox=True, frame=1, threads=8)
     assert not np.array_equal(rp1, rp)
+
+
+def test_sphere_uv_acos_atan2_are_accurate_and_ieee_signed():
+    """GetSphereUV's acos / atan2 (fixed binary32 sequences shared by kernel and oracle, rt_oracle.c): within
+    3 ulp of the double-precision functions, with IEEE atan2's signed-zero quadrants."""
+    import ctypes as C
+    L = po.lib()
+    L.orc_acos.restype, L.orc_acos.argtypes = C.c_float, [C.c_float]
+    L.orc_atan2.restype, L.orc_atan2.argtypes = C.c_float, [C.c_float, C.c_float]
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(-1, 1, 20000), [-1.0, -0.5, 0.0, 0.5, 1.0]]).astype(np.float32)
+    got = np.array([L.orc_acos(float(x)) for x in xs], np.float32)
+    want = np.arccos(xs.astype(np.float64))
+    assert np.all(np.abs(got - want) <= 3 * np.spacing(want.astype(np.float32)))
+    assert L.orc_acos(1.0000001) == 0.0 and L.orc_acos(-1.0000001) == np.float32(np.pi)  # clamped
+    ys, x2 = rng.normal(size=(2, 20000)).astype(np.float32)
+    got = np.array([L.orc_atan2(float(y), float(x)) for y, x in zip(ys, x2)], np.float32)
+    want = np.arctan2(ys.astype(np.float64), x2.astype(np.float64))
+    assert np.all(np.abs(got - want) <= 3 * np.spacing(np.abs(want).astype(np.float32)))
+    pi = np.float32(np.pi)
+    assert [L.orc_atan2(-0.0, -1.0), L.orc_atan2(0.0, -1.0), L.orc_atan2(0.0, -0.0)] == [-pi, pi, pi]
+    assert np.signbit(L.orc_atan2(-0.0, 1.0)) and L.orc_atan2(0.0, 0.0) == 0.0
