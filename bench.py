@@ -1,14 +1,20 @@
 """Headline benchmark: Mray/s of the per-pixel path-trace kernel (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--variant -1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4] [--variant -1] [--tiled-devices 0,0]
 
 A step is one frame of the hot path (Kernel.cu:102-158 → librt_hip.so rt_render) over the whole image;
-inputs (scene tables, RNG state) are resident in HBM before the timed region.  N = 1 renders BASELINE
-config 2 (1920×1080, 64 spp, depth 8, RTIOW final scene).  N > 1 (one process per GPU, launched by
-torch.distributed.run) is weak scaling: the image grows to round(1920·√N) × round(1080·√N) (same camera,
-same field of view, ≈2.07 M pixels per GPU), split in block-cyclic 16-row bands, and every step ends with
-the RCCL gather of the per-rank framebuffers to rank 0.  Rays are counted by the kernel itself (one
-closest-hit query = one iteration of color()'s loop, Kernel.cu:39).
+inputs (scene tables, RNG state) are resident in HBM before the timed region.  Rays are counted by the
+kernel itself (one closest-hit query = one iteration of color()'s loop, Kernel.cu:39).
+
+  --config c2 (default, the BASELINE metric): N = 1 renders config 2 (1920×1080, 64 spp, depth 8, RTIOW
+      final scene).  N > 1 (one process per GPU, launched by torch.distributed.run) is weak scaling: the
+      image grows to round(1920·√N) × round(1080·√N) (same camera and field of view, ≈2.07 M pixels per GPU),
+      split in block-cyclic 16-row bands, and every step ends with the RCCL gather to rank 0.
+  --config c4: BASELINE config 4 as configured, strong scaling: one 7680×4320, 128 spp, depth 8 RTIOW frame
+      split over the N ranks in 16-row bands (N = 1 renders all of it) + the RCCL gather, whose time is
+      reported apart (gather_ms).
+  --tiled-devices d0,d1,…: single process, rt_tiled_* C ABI (one band rank per listed device, peer-copy
+      gather): the path a C++ viewer uses without torch.distributed.
 """
 from __future__ import annotations
 
@@ -37,29 +43,50 @@ F_REF_PER_RAY = 21 * 50.7 + 23 * 6.9 + 60  # reference BVH on C2 (SURVEY.md §8(
 
 
 def cpu_baseline(cfg: scenes.Config, target_s: float) -> dict:
-    """The CPU restatement (oracle/, OpenMP) on a bounded, row-strided sample of the same frame."""
+    """The CPU restatement of the path (oracle/rt_oracle.c built -O3 -march=native -ffp-contract=off on this
+    host, OpenMP over rows; it computes the checker's bits, tests/test_oracle.py) on bounded row-strided samples
+    of the same frame: on the job's whole CPU share, and on one core."""
+    import tempfile
+
     from oracle import py_oracle as po
 
-    threads = min(16, os.cpu_count() or 1)
-    sc = po.OracleScene(scenes.builtin(cfg.scene))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+    except OSError:
+        pass
+    L = po.native_lib(os.path.join(tempfile.gettempdir(), f"rt_oracle_native_{os.getuid()}"))
+    sc = po.OracleScene(scenes.builtin(cfg.scene), library=L)
     inputs = cfg.inputs()
+    st = po.init_states(cfg.width, cfg.height)
 
-    def run(step: int):
-        st = po.init_states(cfg.width, cfg.height)
+    def run(first: int, step: int, nthreads: int):
         t0 = time.perf_counter()
-        _, _, cnt = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, inputs, st, rows=(0, cfg.height),
-                              row_step=step, threads=threads)
-        return cnt.rays, time.perf_counter() - t0
+        _, _, cnt = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, inputs, st, rows=(first, cfg.height),
+                              row_step=step, threads=nthreads, library=L)
+        return cnt.rays, time.perf_counter() - t0, len(range(first, cfg.height, step))
 
-    rays, dt = run(max(1, cfg.height // (4 * threads)))  # calibration: 4 rows per thread
-    rate = rays / max(dt, 1e-6)
-    step = max(1, int(math.ceil(cfg.height * cfg.width * cfg.spp * 3.1 / max(rate * target_s, 1.0))))
-    step = min(step, cfg.height)
-    rays, dt = run(step)
-    nrows = len(range(0, cfg.height, step))
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": f"rows y = 0, {step}, {2 * step}, ... ({nrows} of {cfg.height}) of the {cfg.width}x{cfg.height} "
-                      f"frame at {cfg.spp} spp, depth {cfg.depth}: {rays} rays in {dt:.2f} s, {threads} OpenMP threads"}
+    def sample(first: int, nthreads: int, budget_s: float):
+        step = max(1, cfg.height // (2 * nthreads))  # calibration: ~2 rows per thread
+        for _ in range(3):  # rescale the row stride until the sample takes about budget_s
+            rays, dt, nrows = run(first, step, nthreads)
+            if dt >= 0.5 * budget_s or step == 1:
+                break
+            step = max(1, int(step * dt / budget_s))
+        return rays, dt, nrows, step
+
+    rays, dt, nrows, step = sample(1, threads, target_s)
+    value = rays / dt / 1e6
+    rays1, dt1, nrows1, _ = sample(2, 1, target_s / 3)  # one core: a third of the time budget
+    return {"value": round(value, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "one_core_Mray_s": round(rays1 / dt1 / 1e6, 3), "host_cpus": os.cpu_count(), "cpu_model": model,
+            "build": "gcc -O3 -march=native -ffp-contract=off -fopenmp (oracle/Makefile native), OpenMP over rows",
+            "sample": f"rows y = 1, {1 + step}, {1 + 2 * step}, ... ({nrows} of {cfg.height}) of the {cfg.width}x{cfg.height} "
+                      f"frame at {cfg.spp} spp, depth {cfg.depth}: {rays} rays in {dt:.2f} s on {threads} threads "
+                      f"(the job's CPU share; the host has {os.cpu_count()}); one core: {nrows1} rows, {rays1} rays in "
+                      f"{dt1:.2f} s"}
 
 
 def philox_mode(cfg: scenes.Config, scene: DeviceScene, inputs, steps: int) -> dict:
@@ -97,12 +124,44 @@ def pmc_profile(config: str, rng: str) -> dict:
     return {k: d[k] for k in keys if k in d}
 
 
+def run_tiled(args, cfg: scenes.Config) -> None:
+    """--tiled-devices: one process, rt_tiled_* (band rank r on devices[r], peer-copy gather into one frame)."""
+    from cudaraytracer_amd.renderer import TiledRenderer
+
+    devices = [int(d) for d in args.tiled_devices.split(",")]
+    lib().rt_set_variant(args.variant)
+    t = TiledRenderer(cfg.width, cfg.height, devices, scenes.builtin(cfg.scene), band_rows=16, rng=args.rng)
+    inputs = cfg.inputs()
+    for _ in range(args.warmup):
+        t.render(cfg.spp, cfg.depth, inputs)
+    render_ms, gather_ms, rays = [], [], 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        t.render(cfg.spp, cfg.depth, inputs)
+        render_ms.append(t.timing.render_ms)
+        gather_ms.append(t.timing.gather_ms)
+        rays += t.timing.rays
+    elapsed = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": f"Mray/s at {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}, random-spheres "
+                  f"(single-process rt_tiled C-ABI split)",
+        "value": round(rays / elapsed / 1e6, 2), "unit": "Mray/s", "n_gpus": len(set(devices)),
+        "band_ranks": len(devices), "devices": devices, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "rng": args.rng, "data": "synthetic: RTIOW final scene, glibc rand() seed 1",
+        "config": {"workload": f"{args.config}: {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}",
+                   "parallelism": f"{len(devices)} band ranks (rt_tiled), 16-row bands, peer-copy gather"},
+        "render_ms": round(sum(render_ms) / len(render_ms), 3), "gather_ms": round(sum(gather_ms) / len(gather_ms), 3),
+    }), flush=True)
+    t.close()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--config", default="c2", choices=("c2", "c4"))
     ap.add_argument("--variant", type=int, default=-1, help="kernel variant (rt_set_variant); -1 = automatic")
     ap.add_argument("--rng", choices=("xorwow", "philox"), default="xorwow",
                     help="xorwow: the reference's per-pixel cuRAND state (parity mode, headline); philox: stateless "
@@ -113,7 +172,13 @@ def main() -> None:
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank renders on device 0 (use with --backend gloo)")
+    ap.add_argument("--tiled-devices", default="",
+                    help="single-process multi-device split through the rt_tiled C ABI, e.g. 0,1,2,3 (or 0,0 on one GPU)")
     args = ap.parse_args()
+
+    if args.tiled_devices:
+        run_tiled(args, scenes.CONFIGS[args.config])
+        return
 
     rank, world, local_rank = parallel.env_rank()
     if world != args.gpus:
@@ -125,7 +190,8 @@ def main() -> None:
         parallel.init_process_group(args.backend)
     red_dev = torch.device("cpu") if args.backend == "gloo" else torch.device("cuda", device)
     cfg = scenes.CONFIGS[args.config]
-    if world > 1:
+    strong = args.config == "c4"  # one fixed frame split over the ranks
+    if world > 1 and not strong:
         s = math.sqrt(world)
         cfg = cfg.scaled(int(round(cfg.width * s)), int(round(cfg.height * s)))
     lib().rt_set_variant(args.variant)
@@ -155,7 +221,7 @@ def main() -> None:
         dist.barrier()
     r.counters.zero_()
     stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -166,26 +232,30 @@ def main() -> None:
         ev[i][1].record(stream)
         if world > 1:
             parallel.gather_bands(r.pos, cfg.width, cfg.height, band)
+        ev[i][2].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kernel_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
+    gather_ms = sum(b.elapsed_time(g) for _, b, g in ev) / args.steps
     rays = int(r.counters[0].item())
-    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=red_dev)
+    stats = torch.tensor([elapsed, kernel_ms, gather_ms], dtype=torch.float64, device=red_dev)
     tot = torch.tensor([rays, f_launch], dtype=torch.int64, device=red_dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed, kernel_ms = float(stats[0]), float(stats[1])
+    elapsed, kernel_ms, gather_ms = float(stats[0]), float(stats[1]), float(stats[2])
     rays_all = int(tot[0])
 
     if rank == 0:
         achieved = f_launch / (kernel_ms * 1e-3) / 1e12
-        pmc = pmc_profile(args.config, args.rng) if args.config == "c2" else {}
+        pmc = pmc_profile(args.config, args.rng) if args.config == "c2" and world == 1 else {}
         rays_per_launch = c[0]
+        metric = ("Mray/s (and ms/frame) at 1920x1080, 64 spp, depth 8, random-spheres" if not strong else
+                  "Mray/s (and ms/frame) at 7680x4320, 128 spp, depth 8, random-spheres (8-GPU tile-split config)")
         line = {
-            "metric": "Mray/s (and ms/frame) at 1920x1080, 64 spp, depth 8, random-spheres",
+            "metric": metric,
             "value": round(rays_all / elapsed / 1e6, 2),
             "unit": "Mray/s",
             "n_gpus": world,
@@ -193,7 +263,7 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "rng": args.rng,
@@ -202,11 +272,12 @@ def main() -> None:
                 "workload": (f"{args.config}: {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}, "
                              f"{scenes.CONFIGS[args.config].description.split(', ', 3)[-1]}"),
                 "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
-                "parallelism": f"{world} rank(s) x 16-row bands + gather" if world > 1 else "1 GPU",
+                "parallelism": f"{world} rank(s) x 16-row bands + RCCL gather" if world > 1 else "1 GPU",
                 "kernel_variant": args.variant,
             },
             "kernel_ms": round(kernel_ms, 3),
-            "rays_per_frame": rays_per_launch,
+            "gather_ms": round(gather_ms, 3) if world > 1 else 0.0,
+            "rays_per_frame": rays_all // args.steps,
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved, 3),
@@ -226,11 +297,12 @@ def main() -> None:
                 "flop_per_ray_ref_bvh": round(F_REF_PER_RAY, 1),
                 "box_tests_per_ray": round(c[1] / max(1, c[0]), 2),
                 "prim_tests_per_ray": round(c[2] / max(1, c[0]), 2),
+                "rays_per_launch_rank0": rays_per_launch,
             },
         }
-        if world == 1 and args.rng == "xorwow" and not args.no_philox_line:
+        if world == 1 and args.rng == "xorwow" and not args.no_philox_line and not strong:
             line["philox_mode"] = philox_mode(cfg, scene, inputs, args.steps)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not strong:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1384,7 +1384,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         uint32_t* st = P.state + pix * 12;
         R rng = begin_rng<R>(st, g * P.width + x);  // global pixel index (Kernel.cu:119)
         f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
-        uint32_t sample = (uint32_t)-1, depth = 0, rays = 0;
+        // (sample = -1: v3_next_sample starts sample 0; with spp = 0 it stays 0, so compact parking's packed
+        // sample field cannot spill into the ray count)
+        uint32_t sample = P.spp > 0 ? (uint32_t)-1 : 0u, depth = 0, rays = 0;
         if (P.spp > 0) v3_next_sample(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
         v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);  // (col + 0 = +0 above)
     }

@@ -33,12 +33,29 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
+_native = {}
+
+
+def native_lib(out_dir: str) -> C.CDLL:
+    """The -O3 -march=native build of the same source (CPU baseline, `make -C oracle native`), built into
+    out_dir on the host that runs it."""
+    if out_dir not in _native:
+        subprocess.run(["make", "-s", "-C", HERE, "native", f"NATIVE_OUT={out_dir}"], check=True)
+        _native[out_dir] = _declare(C.CDLL(os.path.join(out_dir, "liboracle.so")))
+    return _native[out_dir]
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
-        L = C.CDLL(LIB_PATH)
+        _lib = _declare(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def _declare(L: C.CDLL) -> C.CDLL:
+    if True:
         vp = C.c_void_p
         L.orc_curand_init.argtypes = [C.c_ulonglong, vp]
         L.orc_curand.argtypes = [vp]
@@ -65,19 +82,19 @@ def lib() -> C.CDLL:
                                   C.POINTER(C.c_float), C.POINTER(C.c_int), C.c_int]
         L.orc_rgb_to_int.argtypes = [C.c_float, C.c_float, C.c_float]
         L.orc_rgb_to_int.restype = C.c_uint
-        _lib = L
-    return _lib
+    return L
 
 
 class OracleScene:
     """exact=False: the reference BVH and its AABB culling (Hittable.cuh:303-439); exact=True: geometric
     closest hit over all active primitives (see orc_scene_set_exact)."""
 
-    def __init__(self, scene, exact: bool = False):
+    def __init__(self, scene, exact: bool = False, library: C.CDLL | None = None):
         self.scene = scene
+        self._lib = library or lib()
         self._desc = scene.desc()
-        self.handle = lib().orc_scene_build(C.byref(self._desc))
-        lib().orc_scene_set_exact(self.handle, 1 if exact else 0)
+        self.handle = self._lib.orc_scene_build(C.byref(self._desc))
+        self._lib.orc_scene_set_exact(self.handle, 1 if exact else 0)
 
     @property
     def depth(self) -> int:
@@ -85,7 +102,7 @@ class OracleScene:
 
     def __del__(self):
         try:
-            lib().orc_scene_free(self.handle)
+            self._lib.orc_scene_free(self.handle)
         except Exception:
             pass
 
@@ -99,7 +116,7 @@ def init_states(width: int, height: int, seed_base: int = 1984, full: bool = Tru
 def render(oscene: OracleScene, width: int, height: int, spp: int, depth: int, inputs: abi.InputStruct,
            states: np.ndarray, faithful_grid: bool = False, rows: tuple | None = None, threads: int = 0,
            rius_order: int = 1, radiance: bool = False, row_step: int = 1, philox: bool = False,
-           seed: int = 1984, frame: int = 0, accum: np.ndarray | None = None):
+           seed: int = 1984, frame: int = 0, accum: np.ndarray | None = None, library: C.CDLL | None = None):
     """One frame; returns (pos (H, W) uint32, radiance (H, W, 4) or None, Counters).  `states` advances
     (XORWOW mode); with philox=True the pixels draw from their (seed, pixel, frame) Philox streams and
     `states` may be None.  `accum` (H·W·4 float32, updated in place): progressive accumulation
@@ -110,7 +127,7 @@ def render(oscene: OracleScene, width: int, height: int, spp: int, depth: int, i
     rad = np.zeros(width * height * 4, dtype=np.float32) if radiance else None
     cnt = Counters()
     r0, r1 = rows if rows else (0, height)
-    lib().orc_render(oscene.handle, pos.ctypes.data, rad.ctypes.data if rad is not None else None,
+    (library or lib()).orc_render(oscene.handle, pos.ctypes.data, rad.ctypes.data if rad is not None else None,
                      accum.ctypes.data if accum is not None else None, width, height,
                      spp, depth, states.ctypes.data if states is not None else None, C.byref(inputs),
                      1 if faithful_grid else 0, r0, r1, row_step, threads, rius_order, 1 if philox else 0, seed, frame,

@@ -332,3 +332,18 @@ def test_sphere_uv_acos_atan2_are_accurate_and_ieee_signed():
     pi = np.float32(np.pi)
     assert [L.orc_atan2(-0.0, -1.0), L.orc_atan2(0.0, -1.0), L.orc_atan2(0.0, -0.0)] == [-pi, pi, pi]
     assert np.signbit(L.orc_atan2(-0.0, 1.0)) and L.orc_atan2(0.0, 0.0) == 0.0
+
+
+def test_native_cpu_baseline_build_computes_the_checker_bits(tmp_path):
+    """The CPU baseline (oracle at -O3 -march=native, still without FP contraction) renders
+    exactly the checker build's image, so the baseline times the same computation."""
+    L = po.native_lib(str(tmp_path / "native"))
+    cfg = scenes.CONFIGS["c2"].scaled(64, 40, 4)
+    sc = scenes.builtin(cfg.scene)
+    st_a, st_b = po.init_states(cfg.width, cfg.height), po.init_states(cfg.width, cfg.height)
+    a, _, ca = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st_a)
+    b, _, cb = po.render(po.OracleScene(sc, library=L), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st_b,
+                         library=L, threads=4)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(st_a, st_b)
+    assert ca.rays == cb.rays
