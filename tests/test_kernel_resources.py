@@ -18,10 +18,11 @@ LIB = os.path.join(ROOT, "cudaraytracer_amd", "librt_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 # render_kernel_v3<COUNT_TESTS=false, W=1, TEX, PHILOX, COMPACT> (variants 2 and 3)
-# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX> (variant 4)
+# render_kernel_v4<COUNT_TESTS=false, TEX, NODES, PHILOX, COMPACT> (variant 4: NODES_64=2; 5: NODES_48=0, compact)
 HOT = [f"_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb{t}ELb{p}ELb{c}EEEvNS0_7KParamsE"
        for t in (0, 1) for p in (0, 1) for c in (0, 1)] + \
-      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}EEEvNS0_7KParamsE" for t in (0, 1) for p in (0, 1)]
+      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi{n}ELb{p}ELb{c}EEEvNS0_7KParamsE"
+       for t in (0, 1) for p in (0, 1) for n, c in ((2, 0), (0, 1))]
 
 
 def kernel_metadata(tmp_path):
