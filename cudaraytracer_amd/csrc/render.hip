@@ -1482,8 +1482,8 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
     return true;
 }
 
-template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool COMPACT = false>
-__global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
+template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool COMPACT = false, int WAVES_PER_SIMD = 1>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
@@ -1728,6 +1728,8 @@ struct Variant {
 constexpr Variant kVariants[] = {
     {dev::STACK_SCRATCH, 0, 256, 1, false}, {dev::STACK_LDS, 24, 64, 2, false}, {dev::STACK_LDS16, 0, 64, 3, false},
     {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false}, {dev::STACK_LDS16, 0, 64, 4, true},
+    // experiment: 5 held to 6 / 7 waves per SIMD by registers
+    {dev::STACK_LDS16, 0, 64, 4, true},     {dev::STACK_LDS16, 0, 64, 4, true},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4, kVarV4Compact = 5;
@@ -1738,10 +1740,10 @@ KernelFn v3_pick(bool count, bool tex) {
     return count ? dev::render_kernel_v3<true, W, false, PH, C> : dev::render_kernel_v3<false, W, false, PH, C>;
 }
 
-template <int N, bool PH = false, bool C = false>
+template <int N, bool PH = false, bool C = false, int W = 1>
 KernelFn v4_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v4<true, true, N, PH, C> : dev::render_kernel_v4<false, true, N, PH, C>;
-    return count ? dev::render_kernel_v4<true, false, N, PH, C> : dev::render_kernel_v4<false, false, N, PH, C>;
+    if (tex) return count ? dev::render_kernel_v4<true, true, N, PH, C, W> : dev::render_kernel_v4<false, true, N, PH, C, W>;
+    return count ? dev::render_kernel_v4<true, false, N, PH, C, W> : dev::render_kernel_v4<false, false, N, PH, C, W>;
 }
 
 #ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the non-texture Philox build of variant 3
@@ -1761,8 +1763,10 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
         return v3_pick<1, false, true>(count, tex);
     case kVarV4:
         return philox ? v4_pick<dev::NODES_64, true>(count, tex) : v4_pick<dev::NODES_64, false>(count, tex);
-    default:
+    case kVarV4Compact:
         return philox ? v4_pick<dev::NODES_48, true, true>(count, tex) : v4_pick<dev::NODES_48, false, true>(count, tex);
+    case 6: return philox ? v4_pick<dev::NODES_48, true, true, 6>(count, tex) : v4_pick<dev::NODES_48, false, true, 6>(count, tex);
+    default: return philox ? v4_pick<dev::NODES_48, true, true, 7>(count, tex) : v4_pick<dev::NODES_48, false, true, 7>(count, tex);
     }
 }
 
@@ -1789,7 +1793,9 @@ struct PlanKey {
     int device;
     void* stream;
     uint32_t tiles_x, tiles;
+    int kind;  // kernel family
     bool operator<(const PlanKey& o) const {
+        if (kind != o.kind) return kind < o.kind;
         if (device != o.device) return device < o.device;
         if (stream != o.stream) return stream < o.stream;
         if (tiles_x != o.tiles_x) return tiles_x < o.tiles_x;
@@ -2082,7 +2088,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u;
     if (kVariants[variant].compact && !packable)  // packed counters would overflow
         variant = kVariants[variant].kernel == 4 ? kVarV4 : kVarV3;
-    if (variant == kVarV4Compact && (a->width >= 65536u || T.local_rows >= 65536u))
+    if (kVariants[variant].kernel == 4 && kVariants[variant].compact && (a->width >= 65536u || T.local_rows >= 65536u))
         variant = kVarV4;  // packed pixel coordinates need 16 bits each
     if (kVariants[variant].kernel == 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
         variant = kVarV3;  // the persistent kernel assumes every pixel traces a ray
@@ -2137,10 +2143,11 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
     P.num_tiles = tiles;
     std::shared_ptr<TilePlan> plan;
-    if ((V.kernel == 3 || variant == kVarV4Compact) && g_adaptive_order && !g_tile_order) {
+    if ((V.kernel == 3 || (persistent && V.compact)) && g_adaptive_order && !g_tile_order) {
         int device = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
-        if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles}, s, &plan);
+        // v3 and v4 measure different costs (wave lifetimes / summed pixel ray counts): separate plans
+        if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles, V.kernel}, s, &plan);
         if (rc == RT_OK && persistent)  // v4 accumulates per-pixel ray counts into its tiles' costs
             rc = hip_check(hipMemsetAsync(plan->cost, 0, (size_t)tiles * 4, s), "rt_render: tile cost reset");
         if (rc != RT_OK) return rc;

@@ -21,7 +21,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 # render_kernel_v4<COUNT_TESTS=false, TEX, NODES, PHILOX, COMPACT> (variant 4: NODES_64=2; 5: NODES_48=0, compact)
 HOT = [f"_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb{t}ELb{p}ELb{c}EEEvNS0_7KParamsE"
        for t in (0, 1) for p in (0, 1) for c in (0, 1)] + \
-      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi{n}ELb{p}ELb{c}EEEvNS0_7KParamsE"
+      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi{n}ELb{p}ELb{c}ELi1EEEvNS0_7KParamsE"
        for t in (0, 1) for p in (0, 1) for n, c in ((2, 0), (0, 1))]
 
 
