@@ -135,6 +135,35 @@ __device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
     return p;
 }
 
+// The same attempts under a wave-level budget (v3): once fewer than `defer_below` of the wave's searching
+// lanes still need another attempt (and at least one attempt ran), the loop stops and returns false for
+// those lanes.  Their RNG has consumed exactly the attempts made; the caller leaves them in the shading
+// state, and at the next shading pass they recompute the same hit record and continue with the next
+// attempt — the same draws in the same order, so the same q.  The rejection loop's wave-level trip count
+// is the maximum over its lanes (~7.9 for 64 lanes at p = 0.524), most of it spent on a few lanes; the
+// tail now runs alongside the next pass's first attempts.  defer_below = 0: never stop early.
+template <class R>
+__device__ __forceinline__ bool random_in_unit_sphere_bounded(R& s, bool rtl, uint32_t defer_below, f3& out) {
+    bool pending = true, first = true;
+    while (true) {
+        const uint64_t m = __ballot(pending);
+        if (m == 0) break;
+        if (!first && (uint32_t)__popcll(m) < defer_below) break;
+        first = false;
+        if (pending) {
+            float a, b, c;
+            draw3(s, a, b, c);
+            const f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
+            const f3 p = sub(scale(2.0f, r), mk(1.0f, 1.0f, 1.0f));
+            if (!(p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f)) {
+                out = p;
+                pending = false;
+            }
+        }
+    }
+    return !pending;
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Kernel parameters (by value; everything launch-uniform precomputed on the host with the same
 // binary32 operations the reference performs per thread).
@@ -174,6 +203,7 @@ struct KParams {
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
+    uint32_t defer_below;            // v3: RandomInUnitSphere's wave-level budget (random_in_unit_sphere_bounded)
 };
 
 constexpr int kStackMax = 64;
@@ -207,6 +237,13 @@ __device__ __forceinline__ uint32_t wave_leader() {
 
 constexpr int kEmpty = (int)0x80000000;
 constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX, rec) (Kernel.cu:40)
+// Conservative box culling.  A slab distance (plane - o)·(1/d) computed as fma(plane, rcp(d), -o·rcp(d)), with
+// rcp within 1 ulp, differs from the exact one by at most ~3·2^-24 of itself plus ~2^-24·|plane·rcp(d)|.  The
+// second term is covered by the host's outward box padding (1e-5 of the plane coordinate, scene_build.cpp);
+// the first grows with the distance travelled, so the far side of every slab interval is widened by a
+// relative 2^-20 (≥ 2·(3·2^-24)): a box the exact ray meets is never culled, whatever the camera distance.
+// (Widening only adds box visits; the closest hit is decided by the exact primitive tests.)
+constexpr float kSlabSlack = 1.0f + 0x1p-20f;
 
 // Closest hit (BVHNode::Hit, Hittable.cuh:387-439, and the primitive tests of PerformHit :470-485).
 // Returns the primitive index (BVH order) or -1, and the hit distance in t_best.
@@ -240,9 +277,9 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
             const float b2 = __builtin_fmaf(n1.z, invd.y, -oiy), b3 = __builtin_fmaf(n1.w, invd.y, -oiy);
             const float b4 = __builtin_fmaf(n2.z, invd.z, -oiz), b5 = __builtin_fmaf(n2.w, invd.z, -oiz);
             const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
-            const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+            const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best)) * kSlabSlack;
             const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
-            const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+            const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best)) * kSlabSlack;
             if (COUNT) {
                 cnt.boxes += 2;
                 cnt.wnode += wave_leader();
@@ -424,11 +461,14 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 }
 
 // One iteration of color()'s bounce loop after the closest-hit query (Kernel.cu:40-76): sky on a miss,
-// emission, or Scatter of the hit material.  Returns true when the path ended (contribution in `contrib`,
-// `emitted * cur_attenuation` or `cur_attenuation * sky`); false when it continues with (ro, rd, att).
+// emission, or Scatter of the hit material.  Returns SHADE_ENDED when the path ended (contribution in
+// `contrib`, `emitted * cur_attenuation` or `cur_attenuation * sky`), SHADE_CONTINUE when it continues with
+// (ro, rd, att), SHADE_DEFERRED when RandomInUnitSphere's wave-level budget ran out for this lane
+// (defer_below > 0): ro, rd and att are untouched and the lane repeats this call at the next shading pass.
+enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1, SHADE_DEFERRED = 2 };
 template <bool TEX = true, class PP, class R>
-__device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
-                                      f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
+__device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
+                                     f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib, uint32_t defer_below = 0) {
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
     // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
     // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
@@ -440,7 +480,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         const float tt = 0.5f * (rd.y / length(rd) + 1.0f);
         const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
         contrib = mulv(att, c);
-        return true;
+        return SHADE_ENDED;
     }
     const float4 p0 = prims[2 * hit + 0];
     const float4 p1 = prims[2 * hit + 1];
@@ -481,7 +521,7 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
         }
         const f3 e = scale(m0.z, tex);
         contrib = mulv(e, att);
-        return true;
+        return SHADE_ENDED;
     }
     float len = 1.0f;
     f3 ud = mk(0.0f, 0.0f, 0.0f);
@@ -520,9 +560,10 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
             rd = mk(0.0f, 0.0f, 0.0f);  // uninitialised `refracted` in the reference (ξ = 1.0, TIR)
         }
         ro = p;
-        return false;
+        return SHADE_CONTINUE;
     }
-    const f3 q = random_in_unit_sphere(rng, rtl);
+    f3 q;
+    if (!random_in_unit_sphere_bounded(rng, rtl, defer_below, q)) return SHADE_DEFERRED;
     const float4 m1 = P->mats[3 * mat + 1];
     f3 attenuation;
     bool ok = true;
@@ -543,10 +584,10 @@ __device__ __forceinline__ bool shade(PP P, const float4* __restrict__ prims, in
     ro = p;
     if (ok) {
         att = mulv(attenuation, att);
-        return false;
+        return SHADE_CONTINUE;
     }
     contrib = mulv(mk(0.0f, 0.0f, 0.0f), att);  // emitted * cur_attenuation
-    return true;
+    return SHADE_ENDED;
 }
 
 // Pixel epilogue (Kernel.cu:149-157): RNG state store, average, gamma 2, RGBA8 pack; optional outputs.
@@ -792,7 +833,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
                 float t;
                 const int hit = trace<COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, cnt);
                 if (COUNT_TESTS) cnt.wshade += wave_leader();
-                done = shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib);
+                done = shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
                 if (!done) depth++;
             }
             if (done) {
@@ -903,9 +944,9 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
                     const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
                     const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
                     const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
-                    const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best));
+                    const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best)) * kSlabSlack;
                     const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
-                    const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best));
+                    const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best)) * kSlabSlack;
                     if (COUNT_TESTS) {
                         cnt.boxes += 2;
                         cnt.wnode += wave_leader();
@@ -990,7 +1031,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
         if (mode == MODE_SHADE) {
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            if (shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t_best, ro, rd, att, rng, rtl, contrib)) {
+            if (shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED) {
                 next_sample(contrib);
             } else if (++depth >= P.max_depth) {
                 next_sample(mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
@@ -1181,6 +1222,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     const f3 pc = mk(invd.x < 0.0f ? invd.x : 0.0f, invd.y < 0.0f ? invd.y : 0.0f, invd.z < 0.0f ? invd.z : 0.0f);
     const uint16_t* ustk = (const uint16_t*)stk;
     while (node != (uint32_t)kSentinel16 || leaf >= 0x8000u) {
+        // t_best changes only in the leaf phase: canonicalised once here, not on every visit by fminf
+        const float t_best_c = __builtin_canonicalizef(t_best);
         while (node < (uint32_t)kSentinel16) {
             const uint32_t top1 = ustk[(sp - 1u) * 64];
             const uint32_t top2 = ustk[(sp - 2u) * 64];
@@ -1205,9 +1248,9 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 const float nz1 = __builtin_fmaf(n2.z, pa.z, __builtin_fmaf(n2.w, pc.z, -oi.z));
                 const float fz1 = __builtin_fmaf(n2.w, pa.z, __builtin_fmaf(n2.z, pc.z, -oi.z));
                 c0min = fmaxf(fmaxf(nx0, ny0), fmaxf(nz0, kTmin));
-                c0max = fminf(fminf(fx0, fy0), fminf(fz0, t_best));
+                c0max = fminf(fminf(fx0, fy0), fminf(fz0, t_best_c)) * kSlabSlack;
                 c1min = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, kTmin));
-                c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best));
+                c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best_c)) * kSlabSlack;
             };
             if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
                 const uint32_t noff = (uint32_t)node << 6;
@@ -1402,6 +1445,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
+        // lanes left to shade later only while other lanes still trace (a later shading pass is coming)
+        const uint32_t defer_below = __ballot(c.mode == MODE_TRAV) != 0 ? P.defer_below : 0u;
         if (c.mode == MODE_SHADE) {
             R rng;
             f3 col, att;
@@ -1409,15 +1454,19 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib);
-            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
-                ended = true;
-                contrib = mk(0.0f, 0.0f, 0.0f);
-            }
-            if (ended) {
-                v3_next_sample(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
-            } else {
-                v3_start_trace(P.num_nodes, c, rays);
+            const int sr = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib,
+                                      defer_below);
+            if (sr != SHADE_DEFERRED) {  // deferred: RandomInUnitSphere continues at the next pass
+                bool ended = sr == SHADE_ENDED;
+                if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+                    ended = true;
+                    contrib = mk(0.0f, 0.0f, 0.0f);
+                }
+                if (ended) {
+                    v3_next_sample(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
+                } else {
+                    v3_start_trace(P.num_nodes, c, rays);
+                }
             }
             v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);
         }
@@ -1520,7 +1569,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
             v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib);
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
             if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
@@ -1771,6 +1820,7 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
 }
 
 thread_local int g_regen_threshold = 40;
+thread_local int g_scatter_defer = 8;  // RT_TUNE_SCATTER_DEFER
 thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupancy experiments)
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
@@ -1938,6 +1988,15 @@ int rt_set_tuning(int key, int value) {
         g_adaptive_order = value;
         return prev;
     }
+    if (key == RT_TUNE_SCATTER_DEFER) {
+        if (value < 0 || value > 64) {
+            set_error("rt_set_tuning: scatter defer threshold must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_scatter_defer;
+        g_scatter_defer = value;
+        return prev;
+    }
     if (key == RT_TUNE_TEXEL_LAYOUT) {
         if (value != 3 && value != 4) {
             set_error("rt_set_tuning: texel layout must be 3 (RGB8) or 4 (RGBA8)");
@@ -2025,6 +2084,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.grid_h = faithful ? (a->height / 16) * 16 : a->height;
     P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
     P.regen_threshold = (uint32_t)g_regen_threshold;
+    P.defer_below = (uint32_t)g_scatter_defer;
     P.rng_key_lo = (uint32_t)a->rng_seed;
     P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
     P.rng_frame = a->rng_frame;

@@ -23,9 +23,12 @@
 //             bytes per texel) as int4, offset -1 = no data
 //
 // Box padding: child boxes are the reference's primitive boxes (Hittable.cuh:112-116, 171-181, ...)
-// grown outward by a relative epsilon, so the fused-multiply-add slab test of the kernel can never
-// reject a primitive the exact test would accept.  Boxes only cull: the closest hit is decided by the
-// primitive tests, which follow the reference arithmetic exactly.
+// grown outward by 1e-5 of the plane coordinate + 1e-6.  That covers the slab test's error term that scales
+// with the plane coordinate (~2^-24·|plane/d|); the term that scales with the distance along the ray is
+// covered in the kernel by widening every slab interval's far side by a relative 2^-20 (kSlabSlack,
+// render.hip), so culling stays conservative for any camera distance (tests/test_gpu_parity.py,
+// far-camera brute-force check).  Boxes only cull: the closest hit is decided by the primitive tests,
+// which follow the reference arithmetic exactly.
 #pragma once
 
 #include <cstdint>
