@@ -105,7 +105,12 @@ __device__ __forceinline__ float uniform(Rng& s) {
     s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
     s.d += 362437u;
     uint32_t x = s.v4 + s.d;
+    // x·2^-32 + 2^-33 (_curand_uniform): the product is exact, so one fma rounds like the mul + add
+#ifdef RT_NO_FMA_UNIFORM
     return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
+#else
+    return __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f / 2.0f);
+#endif
 }
 
 // RandomInUnitSphere (Math.cuh:252-260) with Random() (Math.cuh:231-234).  rtl: the components of
@@ -123,45 +128,33 @@ template <class R> __device__ __forceinline__ void draw3(R& s, float& a, float& 
     c = uniform(s);
 }
 
-template <class R>
-__device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
+// 2·ξ − 1 of each component with one fma: 2·ξ is exact, so it rounds like the reference's mul + sub.  The
+// fill order is a launch-uniform branch around the loop, not a select per attempt.
+template <bool RTL, class R>
+__device__ __forceinline__ f3 random_in_unit_sphere_order(R& s) {
     f3 p;
     do {
         float a, b, c;
         draw3(s, a, b, c);
-        f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
-        p = sub(scale(2.0f, r), mk(1.0f, 1.0f, 1.0f));
+        const f3 r = RTL ? mk(c, b, a) : mk(a, b, c);
+        p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
     } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
     return p;
 }
-
-// The same attempts under a wave-level budget (v3): once fewer than `defer_below` of the wave's searching
-// lanes still need another attempt (and at least one attempt ran), the loop stops and returns false for
-// those lanes.  Their RNG has consumed exactly the attempts made; the caller leaves them in the shading
-// state, and at the next shading pass they recompute the same hit record and continue with the next
-// attempt — the same draws in the same order, so the same q.  The rejection loop's wave-level trip count
-// is the maximum over its lanes (~7.9 for 64 lanes at p = 0.524), most of it spent on a few lanes; the
-// tail now runs alongside the next pass's first attempts.  defer_below = 0: never stop early.
 template <class R>
-__device__ __forceinline__ bool random_in_unit_sphere_bounded(R& s, bool rtl, uint32_t defer_below, f3& out) {
-    bool pending = true, first = true;
-    while (true) {
-        const uint64_t m = __ballot(pending);
-        if (m == 0) break;
-        if (!first && (uint32_t)__popcll(m) < defer_below) break;
-        first = false;
-        if (pending) {
-            float a, b, c;
-            draw3(s, a, b, c);
-            const f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
-            const f3 p = sub(scale(2.0f, r), mk(1.0f, 1.0f, 1.0f));
-            if (!(p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f)) {
-                out = p;
-                pending = false;
-            }
-        }
-    }
-    return !pending;
+__device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
+#ifdef RT_RIUS_BRANCH
+    return rtl ? random_in_unit_sphere_order<true>(s) : random_in_unit_sphere_order<false>(s);
+#else
+    f3 p;
+    do {
+        float a, b, c;
+        draw3(s, a, b, c);
+        const f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
+        p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
+    } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
+    return p;
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -203,7 +196,6 @@ struct KParams {
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
-    uint32_t defer_below;            // v3: RandomInUnitSphere's wave-level budget (random_in_unit_sphere_bounded)
 };
 
 constexpr int kStackMax = 64;
@@ -243,7 +235,10 @@ constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX
 // the first grows with the distance travelled, so the far side of every slab interval is widened by a
 // relative 2^-20 (≥ 2·(3·2^-24)): a box the exact ray meets is never culled, whatever the camera distance.
 // (Widening only adds box visits; the closest hit is decided by the exact primitive tests.)
-constexpr float kSlabSlack = 1.0f + 0x1p-20f;
+#ifndef RT_SLAB_SLACK  // A/B experiments: -DRT_SLAB_SLACK=1.0f disables the widening
+#define RT_SLAB_SLACK (1.0f + 0x1p-20f)
+#endif
+constexpr float kSlabSlack = RT_SLAB_SLACK;
 
 // Closest hit (BVHNode::Hit, Hittable.cuh:387-439, and the primitive tests of PerformHit :470-485).
 // Returns the primitive index (BVH order) or -1, and the hit distance in t_best.
@@ -463,12 +458,11 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 // One iteration of color()'s bounce loop after the closest-hit query (Kernel.cu:40-76): sky on a miss,
 // emission, or Scatter of the hit material.  Returns SHADE_ENDED when the path ended (contribution in
 // `contrib`, `emitted * cur_attenuation` or `cur_attenuation * sky`), SHADE_CONTINUE when it continues with
-// (ro, rd, att), SHADE_DEFERRED when RandomInUnitSphere's wave-level budget ran out for this lane
-// (defer_below > 0): ro, rd and att are untouched and the lane repeats this call at the next shading pass.
-enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1, SHADE_DEFERRED = 2 };
+// (ro, rd, att).
+enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1 };
 template <bool TEX = true, class PP, class R>
 __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
-                                     f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib, uint32_t defer_below = 0) {
+                                     f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
     // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
     // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
@@ -562,8 +556,7 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         ro = p;
         return SHADE_CONTINUE;
     }
-    f3 q;
-    if (!random_in_unit_sphere_bounded(rng, rtl, defer_below, q)) return SHADE_DEFERRED;
+    const f3 q = random_in_unit_sphere(rng, rtl);
     const float4 m1 = P->mats[3 * mat + 1];
     f3 attenuation;
     bool ok = true;
@@ -735,7 +728,7 @@ __device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
 }
 
 __device__ __forceinline__ float philox_to_uniform(uint32_t x) {
-    return 2.3283064e-10f + (float)x * 2.3283064e-10f;  // 2^-32 + x·2^-32 (exact product)
+    return __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f);  // 2^-32 + x·2^-32 (exact product)
 }
 
 // Word j (0..3) of the current block.
@@ -1445,8 +1438,6 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
-        // lanes left to shade later only while other lanes still trace (a later shading pass is coming)
-        const uint32_t defer_below = __ballot(c.mode == MODE_TRAV) != 0 ? P.defer_below : 0u;
         if (c.mode == MODE_SHADE) {
             R rng;
             f3 col, att;
@@ -1454,19 +1445,15 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            const int sr = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib,
-                                      defer_below);
-            if (sr != SHADE_DEFERRED) {  // deferred: RandomInUnitSphere continues at the next pass
-                bool ended = sr == SHADE_ENDED;
-                if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
-                    ended = true;
-                    contrib = mk(0.0f, 0.0f, 0.0f);
-                }
-                if (ended) {
-                    v3_next_sample(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
-                } else {
-                    v3_start_trace(P.num_nodes, c, rays);
-                }
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+                ended = true;
+                contrib = mk(0.0f, 0.0f, 0.0f);
+            }
+            if (ended) {
+                v3_next_sample(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
+            } else {
+                v3_start_trace(P.num_nodes, c, rays);
             }
             v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);
         }
@@ -1795,6 +1782,9 @@ KernelFn v4_pick(bool count, bool tex) {
     return count ? dev::render_kernel_v4<true, false, N, PH, C, W> : dev::render_kernel_v4<false, false, N, PH, C, W>;
 }
 
+#ifndef RT_XORWOW_COMPACT_W  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
+#define RT_XORWOW_COMPACT_W 1
+#endif
 #ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the non-texture Philox build of variant 3
 #define RT_PHILOX_COMPACT_W 1
 #endif
@@ -1809,7 +1799,7 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
         // vs 21.6-21.9 ms, profiles/r01f_ab_philox_w1_w8_c2.txt); -DRT_PHILOX_COMPACT_W=8 rebuilds it
         if (philox)
             return tex ? v3_pick<1, true, true>(count, true) : v3_pick<RT_PHILOX_COMPACT_W, true, true>(count, false);
-        return v3_pick<1, false, true>(count, tex);
+        return v3_pick<RT_XORWOW_COMPACT_W, false, true>(count, tex);
     case kVarV4:
         return philox ? v4_pick<dev::NODES_64, true>(count, tex) : v4_pick<dev::NODES_64, false>(count, tex);
     case kVarV4Compact:
@@ -1820,7 +1810,6 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
 }
 
 thread_local int g_regen_threshold = 40;
-thread_local int g_scatter_defer = 8;  // RT_TUNE_SCATTER_DEFER
 thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupancy experiments)
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
@@ -1988,15 +1977,6 @@ int rt_set_tuning(int key, int value) {
         g_adaptive_order = value;
         return prev;
     }
-    if (key == RT_TUNE_SCATTER_DEFER) {
-        if (value < 0 || value > 64) {
-            set_error("rt_set_tuning: scatter defer threshold must be in [0, 64]");
-            return RT_ERR_INVALID_ARGUMENT;
-        }
-        int prev = g_scatter_defer;
-        g_scatter_defer = value;
-        return prev;
-    }
     if (key == RT_TUNE_TEXEL_LAYOUT) {
         if (value != 3 && value != 4) {
             set_error("rt_set_tuning: texel layout must be 3 (RGB8) or 4 (RGBA8)");
@@ -2084,7 +2064,6 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.grid_h = faithful ? (a->height / 16) * 16 : a->height;
     P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
     P.regen_threshold = (uint32_t)g_regen_threshold;
-    P.defer_below = (uint32_t)g_scatter_defer;
     P.rng_key_lo = (uint32_t)a->rng_seed;
     P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
     P.rng_frame = a->rng_frame;

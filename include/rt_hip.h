@@ -296,12 +296,9 @@ int rt_set_variant(int variant);
 /*   RT_TUNE_TEXEL_LAYOUT: device bytes per texel of the images of later rt_scene_create calls: 3 (default,
  *   the reference's RGB8 layout, Texture.cuh:76: three byte gathers per lookup) or 4 (RGBA8-padded: one dword
  *   gather per lookup, 4/3 the memory).  The image does not depend on it. */
-/*   RT_TUNE_SCATTER_DEFER: v3 kernels: RandomInUnitSphere's rejection loop (Math.cuh:252-260) stops for the
- *   wave once fewer than this many lanes still need another attempt; those lanes continue it at the next
- *   shading pass with the same draws (0 = never; 0..64, default 8).  The image does not depend on it. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
-                     RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_SCATTER_DEFER = 7 };
+                     RT_TUNE_TEXEL_LAYOUT = 6 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

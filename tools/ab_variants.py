@@ -16,7 +16,6 @@ ap.add_argument("--leafmax", default="4", help="BVH leaf sizes to try (RT_TUNE_L
 ap.add_argument("--pwaves", default="0", help="persistent grid waves/SIMD to try (RT_TUNE_PERSISTENT_WAVES)")
 ap.add_argument("--sah", default="12", help="SAH traversal costs x10 to try (RT_TUNE_SAH_TRAVERSAL)")
 ap.add_argument("--rng", default="xorwow", choices=("xorwow", "philox"))
-ap.add_argument("--defer", default="8", help="RandomInUnitSphere wave budgets to try (RT_TUNE_SCATTER_DEFER)")
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
 if args.spp:
@@ -28,8 +27,7 @@ for sah in (int(x) for x in args.sah.split(",")):
         for v in (int(v) for v in args.variants.split(",")):
             for th in [int(t) for t in args.thresholds.split(",")]:
                 for pw in ([int(p) for p in args.pwaves.split(",")] if v == 4 else [0]):
-                    for df in (int(d) for d in args.defer.split(",")):
-                        variants.append((v, th, lm, pw, df))
+                    variants.append((v, th, lm, pw, 0))
 scenes_by_lm = {}
 for lm in sorted({v[2] for v in variants}):
     lib().rt_set_tuning(1, lm[0])
@@ -46,7 +44,6 @@ for v, th, lm, pw, df in variants:  # warm-up / JIT of each variant
     lib().rt_set_variant(v)
     lib().rt_set_tuning(0, th)
     lib().rt_set_tuning(2, pw)
-    lib().rt_set_tuning(7, df)
     r.render(scenes_by_lm[lm], cfg.spp, cfg.depth, inp)
 torch.cuda.synchronize()
 for rnd in range(args.rounds):
@@ -54,7 +51,6 @@ for rnd in range(args.rounds):
         lib().rt_set_variant(v[0])
         lib().rt_set_tuning(0, v[1])
         lib().rt_set_tuning(2, v[3])
-        lib().rt_set_tuning(7, v[4])
         r.counters.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -65,4 +61,4 @@ for rnd in range(args.rounds):
         rays[v] = int(r.counters[0])
 for v in variants:
     med = statistics.median(times[v])
-    print(f"{args.config} {args.rng} variant {v[0]} thr {v[1]} leafmax {v[2][0]} sah {v[2][1]} pwaves {v[3]} defer {v[4]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)
+    print(f"{args.config} {args.rng} variant {v[0]} thr {v[1]} leafmax {v[2][0]} sah {v[2][1]} pwaves {v[3]}: median {med:.2f} ms  min {min(times[v]):.2f}  {rays[v] / med / 1e6:.3f} Gray/s", flush=True)

@@ -6,5 +6,6 @@ OUT=$(realpath -m "$1"); shift
 cd "$(dirname "$0")/../cudaraytracer_amd/csrc"
 T=$(mktemp -d)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-slp-vectorize -mllvm -simplifycfg-sink-common=false "$@" -c render.hip -o $T/render.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" $T/render.o ../../build/obj/api.o ../../build/obj/scene_build.o ../../build/obj/builtin_scenes.o
+make -s -C . >/dev/null  # the host objects the library links (build/obj)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" $T/render.o $(ls ../../build/obj/*.o | grep -v '/render.o$')
 rm -rf $T
