@@ -1490,27 +1490,18 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
 //   result does not depend on which lane or wave renders it.  Every wave exits once the queue is empty
 //   and its lanes are done (no wave waits on another).
 // Requires spp ≥ 1 and max_depth ≥ 1 (rt_render uses v3 otherwise).
-// ORDERED: work chunks (tiles) are taken in the longest-first order planned from the previous launch's
-// per-tile ray counts (each finished pixel adds its rays to its tile's cost), so the frame's last pixels
-// are cheap ones and the device drains evenly.
-// LDS per wave: 18 × 256 B of parked state (15 with compact parking: packed sample/depth/rays, packed
-// pixel coordinates, the lane's ray total) + (depth + 2) × 128 B of stack.
+// LDS per wave: 18 × 256 B of parked state + (depth + 2) × 128 B of stack.
 // ---------------------------------------------------------------------------------------------------
 enum ParkSlotV4 { PK_X = PK_WORDS, PK_G = PK_WORDS + 1, PK_PIX = PK_WORDS + 2, PK_WORDS4 = PK_WORDS + 3 };
-enum ParkSlotV4Compact { PK_XY = PK_WORDS_COMPACT, PK_TOTAL = PK_WORDS_COMPACT + 1, PK_WORDS4_COMPACT = PK_WORDS_COMPACT + 2 };
-__host__ __device__ constexpr int park_words_v4(bool compact) { return compact ? PK_WORDS4_COMPACT : PK_WORDS4; }
 constexpr int MODE_NEED = 3;  // v4: lane waits for a pixel
 
-// Work index → pixel of the local image (8×8 tiles; chunk k of 64 indices is tile order[k], or tile k);
-// false when the index lies outside the image or outside the rendered grid.
-__device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint32_t& x, uint32_t& ly, uint32_t& g,
-                                           uint32_t& pix) {
-    uint32_t tile = idx >> 6;
-    const uint32_t l = idx & 63u;
-    if (P.tile_order) tile = P.tile_order[tile];
+// Work index → pixel of the local image (8×8 tiles, row-major tile order); false when the index lies
+// outside the image or outside the rendered grid.
+__device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint32_t& x, uint32_t& g, uint32_t& pix) {
+    const uint32_t tile = idx >> 6, l = idx & 63u;
     const uint32_t by = tile / P.tiles_x, bx = tile - by * P.tiles_x;
     x = bx * 8u + (l & 7u);
-    ly = by * 8u + (l >> 3);
+    const uint32_t ly = by * 8u + (l >> 3);
     if (x >= P.width || ly >= P.local_rows) return false;
     g = global_row(P, ly);
     if (x >= P.grid_w || g >= P.grid_h) return false;
@@ -1518,14 +1509,14 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
     return true;
 }
 
-template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool COMPACT = false, int WAVES_PER_SIMD = 1>
-__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
+template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false>
+__global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t* const wl = (uint32_t*)lds;
     uint32_t* const park = wl + lane;
-    int16_t* const stk = reinterpret_cast<int16_t*>(wl + park_words_v4(COMPACT) * 64) + lane;
+    int16_t* const stk = reinterpret_cast<int16_t*>(wl + PK_WORDS4 * 64) + lane;
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
                           : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
@@ -1535,7 +1526,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     const bool rtl = P.rius_rtl != 0;
     stk[0] = (int16_t)kSentinel16;
     stk[64] = (int16_t)kSentinel16;
-    park[(COMPACT ? PK_TOTAL : PK_RAYS) * 64] = 0u;
+    park[PK_RAYS * 64] = 0u;
 
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
@@ -1553,7 +1544,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
         bool cam = false, fin = false;
         const bool shading = c.mode == MODE_SHADE;
         if (shading) {
-            v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
+            v3_unpark(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
             bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
@@ -1566,18 +1557,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
                 if (++sample < P.spp) {
                     cam = true;
                 } else {  // the pixel is done (Kernel.cu:149-157)
-                    uint32_t pix, tile;
-                    if constexpr (COMPACT) {
-                        const uint32_t xy = park[PK_XY * 64], x = xy & 0xffffu, ly = xy >> 16;
-                        pix = ly * P.width + x;
-                        tile = (ly >> 3) * P.tiles_x + (x >> 3);
-                        park[PK_TOTAL * 64] += rays;  // the packed field counts this pixel's rays only
-                    } else {
-                        pix = park[PK_PIX * 64];
-                        tile = 0u;  // no cost accounting (the packed per-pixel ray count is compact-only)
-                    }
-                    if (COMPACT && P.tile_cost) atomicAdd(&P.tile_cost[tile], rays);  // the next launch's order
-                    if constexpr (COMPACT) rays = 0u;
+                    const uint32_t pix = park[PK_PIX * 64];
                     write_pixel(P, pix, P.state + (size_t)pix * 12, rng, col);
                     fin = true;
                 }
@@ -1589,7 +1569,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
         bool need = fin || c.mode == MODE_NEED;
         uint64_t needm = __ballot(need);
         if (needm != 0) {
-            if (!shading && need) rays = COMPACT ? 0u : park[PK_RAYS * 64];
+            if (!shading && need) rays = park[PK_RAYS * 64];
             while (needm != 0 && !drained) {
                 if (wq_next >= wq_end) {
                     const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
@@ -1607,16 +1587,12 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
                 const uint32_t rank =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
                 if (need && rank < avail) {
-                    uint32_t x, ly, g, pix;
-                    if (work_pixel(P, wq_next + rank, x, ly, g, pix)) {
+                    uint32_t x, g, pix;
+                    if (work_pixel(P, wq_next + rank, x, g, pix)) {
                         need = false;
-                        if constexpr (COMPACT) {
-                            park[PK_XY * 64] = x | (ly << 16);
-                        } else {
-                            park[PK_X * 64] = x;
-                            park[PK_G * 64] = g;
-                            park[PK_PIX * 64] = pix;
-                        }
+                        park[PK_X * 64] = x;
+                        park[PK_G * 64] = g;
+                        park[PK_PIX * 64] = pix;
                         rng = begin_rng<R>(P.state + (size_t)pix * 12, g * P.width + x);
                         col = mk(0.0f, 0.0f, 0.0f);
                         sample = 0u;
@@ -1633,25 +1609,16 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
         }
         if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
             KParamsC* q = kparams_reload();
-            uint32_t cx, cg;
-            if constexpr (COMPACT) {
-                const uint32_t xy = park[PK_XY * 64];
-                cx = xy & 0xffffu;
-                cg = global_row(P, xy >> 16);
-            } else {
-                cx = park[PK_X * 64];
-                cg = park[PK_G * 64];
-            }
-            const Camera cam_l = lane_camera(q, cx, cg);
+            const Camera cam_l = lane_camera(q, park[PK_X * 64], park[PK_G * 64]);
             camera_ray(q, cam_l, rng, ro, rd);
             att = mk(1.0f, 1.0f, 1.0f);
             depth = 0u;
             v3_start_trace(P.num_nodes, c, rays);
         }
-        if (shading || cam) v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);
+        if (shading || cam) v3_park(park, rng, col, att, sample, depth, rays);
         if (__ballot(c.mode != MODE_DONE) == 0) break;
     }
-    cnt.rays = COMPACT ? park[PK_TOTAL * 64] : park[PK_RAYS * 64];
+    cnt.rays = park[PK_RAYS * 64];
     // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
     cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;
     flush_counts<COUNT_TESTS>(P, cnt);
@@ -1752,8 +1719,9 @@ using KernelFn = void (*)(const dev::KParams);
 //   1  v2: 64-thread resumable, 32-bit LDS stacks — fallback for scenes beyond 16-bit references
 //   2  v3: 15-word parking                        — spp/depth too large for compact parking
 //   3  v3: 13-word compact parking                — default for spp >= 32
-//   4  v4: persistent work queue, 64-B nodes      — round 1's persistent kernel (A/B reference)
-//   5  v4: compact parking, 48-B nodes + scalar uniform nodes, longest-first chunk order — default for spp < 32
+//   4  v4: persistent work queue, 64-B nodes      — default for spp < 32 (a compact-parking, 48-B-node,
+//         longest-first-ordered v4 measured slower on C2, C3 and C5: profiles/r02_ab_v3_v4compact_c2.txt,
+//         profiles/r02_configs_v345.txt)
 struct Variant {
     int stack;        // StackKind
     int lds_depth;    // v2: LDS stack entries per lane
@@ -1763,12 +1731,10 @@ struct Variant {
 };
 constexpr Variant kVariants[] = {
     {dev::STACK_SCRATCH, 0, 256, 1, false}, {dev::STACK_LDS, 24, 64, 2, false}, {dev::STACK_LDS16, 0, 64, 3, false},
-    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false}, {dev::STACK_LDS16, 0, 64, 4, true},
-    // experiment: 5 held to 6 / 7 waves per SIMD by registers
-    {dev::STACK_LDS16, 0, 64, 4, true},     {dev::STACK_LDS16, 0, 64, 4, true},
+    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
-constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4, kVarV4Compact = 5;
+constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4;
 
 template <int W, bool PH = false, bool C = false>
 KernelFn v3_pick(bool count, bool tex) {
@@ -1776,17 +1742,17 @@ KernelFn v3_pick(bool count, bool tex) {
     return count ? dev::render_kernel_v3<true, W, false, PH, C> : dev::render_kernel_v3<false, W, false, PH, C>;
 }
 
-template <int N, bool PH = false, bool C = false, int W = 1>
+template <bool PH = false>
 KernelFn v4_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v4<true, true, N, PH, C, W> : dev::render_kernel_v4<false, true, N, PH, C, W>;
-    return count ? dev::render_kernel_v4<true, false, N, PH, C, W> : dev::render_kernel_v4<false, false, N, PH, C, W>;
+    if (tex) return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH> : dev::render_kernel_v4<false, true, dev::NODES_64, PH>;
+    return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH> : dev::render_kernel_v4<false, false, dev::NODES_64, PH>;
 }
 
 #ifndef RT_XORWOW_COMPACT_W  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
-#define RT_XORWOW_COMPACT_W 1
+#define RT_XORWOW_COMPACT_W 8
 #endif
 #ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the non-texture Philox build of variant 3
-#define RT_PHILOX_COMPACT_W 1
+#define RT_PHILOX_COMPACT_W 7
 #endif
 
 KernelFn pick(int variant, bool count, bool tex, bool philox) {
@@ -1795,17 +1761,13 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
     case kVarV2: return count ? dev::render_kernel_v2<true> : dev::render_kernel_v2<false>;
     case kVarV3: return philox ? v3_pick<1, true>(count, tex) : v3_pick<1>(count, tex);
     case kVarV3Compact:
-        // Philox: W = 8 (64 VGPRs, one cold 8-B spill) lost to W = 1 in a same-box A/B (c2 median 22.5-22.8
-        // vs 21.6-21.9 ms, profiles/r01f_ab_philox_w1_w8_c2.txt); -DRT_PHILOX_COMPACT_W=8 rebuilds it
+        // Waves per SIMD by registers (profiles/r02_ab_builds_c2.txt): XORWOW held to 64 VGPRs (8 waves,
+        // 28 B of cold spills) 16.98 vs 17.25 ms at the compiler's 68; Philox held to 72 (7 waves) 21.5 vs
+        // 21.9 ms at 75, while 8 waves (64 VGPRs, 40 B of spills) ran 22.6 ms
         if (philox)
             return tex ? v3_pick<1, true, true>(count, true) : v3_pick<RT_PHILOX_COMPACT_W, true, true>(count, false);
         return v3_pick<RT_XORWOW_COMPACT_W, false, true>(count, tex);
-    case kVarV4:
-        return philox ? v4_pick<dev::NODES_64, true>(count, tex) : v4_pick<dev::NODES_64, false>(count, tex);
-    case kVarV4Compact:
-        return philox ? v4_pick<dev::NODES_48, true, true>(count, tex) : v4_pick<dev::NODES_48, false, true>(count, tex);
-    case 6: return philox ? v4_pick<dev::NODES_48, true, true, 6>(count, tex) : v4_pick<dev::NODES_48, false, true, 6>(count, tex);
-    default: return philox ? v4_pick<dev::NODES_48, true, true, 7>(count, tex) : v4_pick<dev::NODES_48, false, true, 7>(count, tex);
+    default: return philox ? v4_pick<true>(count, tex) : v4_pick<false>(count, tex);
     }
 }
 
@@ -2125,10 +2087,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
     const bool packable =
         a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u;
-    if (kVariants[variant].compact && !packable)  // packed counters would overflow
-        variant = kVariants[variant].kernel == 4 ? kVarV4 : kVarV3;
-    if (kVariants[variant].kernel == 4 && kVariants[variant].compact && (a->width >= 65536u || T.local_rows >= 65536u))
-        variant = kVarV4;  // packed pixel coordinates need 16 bits each
+    if (kVariants[variant].compact && !packable) variant = kVarV3;  // packed counters would overflow
     if (kVariants[variant].kernel == 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
         variant = kVarV3;  // the persistent kernel assumes every pixel traces a ray
     if (philox && kVariants[variant].stack != dev::STACK_LDS16) {
@@ -2150,7 +2109,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // the far child lands at index 2 + (L - 1) <= depth + 1 (the 128-B saving keeps config 2's wave
     // inside 10 × 512 B of LDS)
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
-                                  ? (size_t)(persistent ? dev::park_words_v4(V.compact) : dev::park_words(V.compact)) * 64 * 4 +
+                                  ? (size_t)(persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
                                         (size_t)(S.depth + 2) * 64 * 2 + (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
@@ -2182,13 +2141,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
     P.num_tiles = tiles;
     std::shared_ptr<TilePlan> plan;
-    if ((V.kernel == 3 || (persistent && V.compact)) && g_adaptive_order && !g_tile_order) {
+    if (V.kernel == 3 && g_adaptive_order && !g_tile_order) {
         int device = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
-        // v3 and v4 measure different costs (wave lifetimes / summed pixel ray counts): separate plans
         if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles, V.kernel}, s, &plan);
-        if (rc == RT_OK && persistent)  // v4 accumulates per-pixel ray counts into its tiles' costs
-            rc = hip_check(hipMemsetAsync(plan->cost, 0, (size_t)tiles * 4, s), "rt_render: tile cost reset");
         if (rc != RT_OK) return rc;
         P.tile_cost = plan->cost;
         P.tile_order = plan->valid.load() ? plan->order : nullptr;

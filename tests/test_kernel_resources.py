@@ -17,12 +17,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "cudaraytracer_amd", "librt_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
-# render_kernel_v3<COUNT_TESTS=false, W=1, TEX, PHILOX, COMPACT> (variants 2 and 3)
-# render_kernel_v4<COUNT_TESTS=false, TEX, NODES, PHILOX, COMPACT> (variant 4: NODES_64=2; 5: NODES_48=0, compact)
-HOT = [f"_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb{t}ELb{p}ELb{c}EEEvNS0_7KParamsE"
-       for t in (0, 1) for p in (0, 1) for c in (0, 1)] + \
-      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi{n}ELb{p}ELb{c}ELi1EEEvNS0_7KParamsE"
-       for t in (0, 1) for p in (0, 1) for n, c in ((2, 0), (0, 1))]
+# render_kernel_v3<COUNT_TESTS=false, W, TEX, PHILOX, COMPACT> (variants 2 and 3; the untextured compact builds
+# are held to 8 (XORWOW) / 7 (Philox) waves per SIMD by registers, render.hip RT_*_COMPACT_W)
+# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX> (variant 4)
+def _v3(t, p, c):
+    w = (8 if not p else 7) if (c and not t) else 1
+    return f"_ZN2rt3dev16render_kernel_v3ILb0ELi{w}ELb{t}ELb{p}ELb{c}EEEvNS0_7KParamsE"
+
+
+HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + \
+      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}EEEvNS0_7KParamsE" for t in (0, 1) for p in (0, 1)]
+# register-held builds: a few bytes of cold spills (measured faster than the compiler's register count)
+SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 16}
 
 
 def kernel_metadata(tmp_path):
@@ -47,13 +53,13 @@ def kernel_metadata(tmp_path):
 
 
 @pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(f"{LLVM}/llvm-readelf")), reason="needs the built library and ROCm LLVM tools")
-def test_hot_kernels_use_no_scratch_and_at_most_72_vgprs(tmp_path):
+def test_hot_kernels_register_and_scratch_budget(tmp_path):
     meta = kernel_metadata(tmp_path)
     for k in HOT:
         assert k in meta, k
-        assert meta[k]["private_segment_fixed_size"] == 0, (k, meta[k])
-        assert meta[k]["vgpr_spill_count"] == 0, (k, meta[k])
-        if "render_kernel_v3ILb0ELi1ELb0E" in k:
+        assert meta[k]["private_segment_fixed_size"] <= SPILL_OK.get(k, 0), (k, meta[k])
+        if "render_kernel_v3ILb0ELi1ELb0ELb0E" in k:  # untextured XORWOW builds
             assert meta[k]["vgpr_count"] <= 72, (k, meta[k])
     # the default kernel of untextured many-sample frames (variant 3, XORWOW) at 8 waves per SIMD
-    assert meta["_ZN2rt3dev16render_kernel_v3ILb0ELi1ELb0ELb0ELb1EEEvNS0_7KParamsE"]["vgpr_count"] <= 64
+    assert meta[_v3(0, 0, 1)]["vgpr_count"] <= 64
+    assert meta[_v3(0, 1, 1)]["vgpr_count"] <= 72
