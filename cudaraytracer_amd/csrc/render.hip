@@ -1766,7 +1766,7 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
         // 21.9 ms at 75, while 8 waves (64 VGPRs, 40 B of spills) ran 22.6 ms
         if (philox)
             return tex ? v3_pick<1, true, true>(count, true) : v3_pick<RT_PHILOX_COMPACT_W, true, true>(count, false);
-        return v3_pick<RT_XORWOW_COMPACT_W, false, true>(count, tex);
+        return tex ? v3_pick<1, false, true>(count, true) : v3_pick<RT_XORWOW_COMPACT_W, false, true>(count, false);
     default: return philox ? v4_pick<true>(count, tex) : v4_pick<false>(count, tex);
     }
 }
