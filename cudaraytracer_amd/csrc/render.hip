@@ -55,10 +55,22 @@ __device__ __forceinline__ f3 scale(float t, f3 v) { return mk(t * v.x, t * v.y,
 __device__ __forceinline__ f3 divs(f3 v, float t) { return mk(v.x / t, v.y / t, v.z / t); }
 __device__ __forceinline__ f3 neg(f3 v) { return mk(-v.x, -v.y, -v.z); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+// sqrtf(x) for x >= 2^-96 (finite or +inf): the instruction sequence LLVM emits for the correctly rounded
+// square root — v_sqrt_f32 and a residual check of its two neighbours — without the small-input scaling
+// and the 0/inf class test, neither of which changes the result in that range (saves ~24 of ~54 cycles).
+__device__ __forceinline__ float sqrt_rn(const float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+    r = __builtin_fmaf(-sup, s, x) > 0.0f ? sup : r;
+    return r;
+}
+// sqrtf(x) bit for bit: sqrt_rn in its range, LLVM's full sequence (a branch no lane usually takes) below it
+__device__ __forceinline__ float sqrt_fast(const float x) { return x >= 0x1p-96f ? sqrt_rn(x) : sqrtf(x); }
+__device__ __forceinline__ float length(f3 v) { return sqrt_fast(v.x * v.x + v.y * v.y + v.z * v.z); }
 __device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, length(v)); }
 __device__ __forceinline__ f3 normalize(f3 v) {
-    float inv = 1.0f / sqrtf(dot(v, v));
+    float inv = 1.0f / sqrt_fast(dot(v, v));
     return scale(inv, v);
 }
 // x / a correctly rounded from y = RN(1/a) (a one-off IEEE division) in five 2-cycle ops instead of the
@@ -102,7 +114,13 @@ __device__ __forceinline__ float uniform(Rng& s) {
     s.v1 = s.v2;
     s.v2 = s.v3;
     s.v3 = s.v4;
+#ifdef RT_XORWOW_SHL
     s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+#else
+    uint32_t t2;  // t << 1 as a full-rate add (v_lshlrev_b32 issues at half rate on gfx950)
+    asm("v_add_u32 %0, %1, %1" : "=v"(t2) : "v"(t));
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ t2);
+#endif
     s.d += 362437u;
     uint32_t x = s.v4 + s.d;
     // x·2^-32 + 2^-33 (_curand_uniform): the product is exact, so one fma rounds like the mul + add
@@ -220,6 +238,9 @@ struct Counts {
     uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
     uint32_t wnode_uniform = 0, wleaf_uniform = 0;  // COUNT_TESTS (v3): ... of them with one node / primitive
     uint64_t ctrav = 0, cshade = 0, ctotal = 0, cleaf = 0;  // COUNT_TESTS (v3): wave clock cycles per phase
+    // COUNT_TESTS (v3): idle lanes summed over node iterations: pixel done / ray finished, waiting for the
+    // regeneration threshold / holding a leaf while the wave still visits nodes
+    uint64_t idle_nt = 0, idle_fin = 0, idle_wait = 0;
 };
 
 // 1 on the lowest active lane of the wave, 0 elsewhere (diagnostic wave-iteration counts).
@@ -622,6 +643,9 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt
             atomicAdd(&P.counters[6], (unsigned long long)cnt.wshade);
             atomicAdd(&P.counters[11], (unsigned long long)cnt.wnode_uniform);
             atomicAdd(&P.counters[12], (unsigned long long)cnt.wleaf_uniform);
+            atomicAdd(&P.counters[13], (unsigned long long)cnt.idle_nt);
+            atomicAdd(&P.counters[14], (unsigned long long)cnt.idle_fin);
+            atomicAdd(&P.counters[15], (unsigned long long)cnt.idle_wait);
             if (cnt.ctotal && wave_leader()) {  // one lane per wave: the stamps are wave-uniform
                 atomicAdd(&P.counters[7], (unsigned long long)cnt.ctrav);
                 atomicAdd(&P.counters[8], (unsigned long long)cnt.cshade);
@@ -1166,22 +1190,24 @@ __device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col,
     }
 }
 
-// sqrtf(x) for x >= 2^-96 (finite or +inf): the instruction sequence LLVM emits for the correctly rounded
-// square root — v_sqrt_f32 and a residual check of its two neighbours — without the small-input scaling
-// and the 0/inf class test, neither of which changes the result in that range (saves ~24 of ~54 cycles).
-__device__ __forceinline__ float sqrt_rn(const float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
-    float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
-    r = __builtin_fmaf(-sup, s, x) > 0.0f ? sup : r;
-    return r;
-}
 
 // Constant-address-space views of the read-only scene buffers: loads from them at wave-uniform indices become
 // scalar loads (s_load_dword*) whose results feed VALU instructions as SGPR operands.
 typedef const __attribute__((address_space(4))) float ConstF32;
 typedef const __attribute__((address_space(4))) uint32_t ConstU32;
 typedef const __attribute__((address_space(4))) uint8_t ConstU8;
+#ifndef RT_SLAB_ASM
+#define RT_SLAB_ASM 1
+#endif
+// v_min/v_max(3)_f32 as plain instructions: the operands are finite FMA results or canonical values
+__device__ __forceinline__ float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(a), "v"(b)); return r; }
+__device__ __forceinline__ float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+__device__ __forceinline__ float vmax3(float a, float b, float c) { float r; asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
+__device__ __forceinline__ float vmin3(float a, float b, float c) { float r; asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
+#ifndef RT_PRIM_BUFFER
+#define RT_PRIM_BUFFER 1
+#endif
+constexpr uint32_t kPrimStep = RT_PRIM_BUFFER ? 32u : 1u;
 #ifndef RT_SCALAR_NODES
 #define RT_SCALAR_NODES 1
 #endif
@@ -1195,7 +1221,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                                             const float4* __restrict__ nodes48, const uint32_t* __restrict__ refs16,
                                             const float4* __restrict__ prims, int16_t* const stk,
                                             const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
-                                            Counts& cnt) {
+                                            Counts& cnt, const uint32_t ntrav = 64) {
     // node / leaf references as unsigned 16-bit values: internal nodes < 0x7fff, kSentinel16 = 0x7fff, leaf
     // references (int16 < 0 in the layout) >= 0x8000; leaf == 0: no postponed leaf
     uint32_t node = (uint32_t)c.node, leaf = (uint32_t)c.leaf;
@@ -1211,15 +1237,27 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
     const f3 oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
-    const f3 pa = mk(invd.x < 0.0f ? 0.0f : invd.x, invd.y < 0.0f ? 0.0f : invd.y, invd.z < 0.0f ? 0.0f : invd.z);
-    const f3 pc = mk(invd.x < 0.0f ? invd.x : 0.0f, invd.y < 0.0f ? invd.y : 0.0f, invd.z < 0.0f ? invd.z : 0.0f);
+    // (invd, 0) or (0, invd) by sign with one max / min each (invd is never NaN; a -0 that became +0
+    // changes only the sign of a zero plane distance, which no comparison sees)
+    const f3 pa = mk(fmaxf(invd.x, 0.0f), fmaxf(invd.y, 0.0f), fmaxf(invd.z, 0.0f));
+    const f3 pc = mk(fminf(invd.x, 0.0f), fminf(invd.y, 0.0f), fminf(invd.z, 0.0f));
     const uint16_t* ustk = (const uint16_t*)stk;
+    const float tmin_s = kTmin;  // an SGPR operand of the slab test's v_max
+#if RT_PRIM_BUFFER
+    const __amdgpu_buffer_rsrc_t prsrc = __builtin_amdgcn_make_buffer_rsrc((void*)prims, (short)0, 0x7fffffff, 0x00020000);
+#endif
     while (node != (uint32_t)kSentinel16 || leaf >= 0x8000u) {
         // t_best changes only in the leaf phase: canonicalised once here, not on every visit by fminf
         const float t_best_c = __builtin_canonicalizef(t_best);
+        const uint32_t n_outer = COUNT_TESTS ? (uint32_t)__popcll(__ballot(1)) : 0u;  // lanes still tracing
+        (void)n_outer;
         while (node < (uint32_t)kSentinel16) {
-            const uint32_t top1 = ustk[(sp - 1u) * 64];
-            const uint32_t top2 = ustk[(sp - 2u) * 64];
+            uint32_t top1 = ustk[(sp - 1u) * 64];
+            uint32_t top2 = ustk[(sp - 2u) * 64];
+            // materialise the zero-extended words here: used in another basic block, the loaded u16 would
+            // otherwise be re-extended there with a v_and per word and visit
+            asm("" : "+v"(top1));
+            asm("" : "+v"(top2));
             float c0min, c0max, c1min, c1max;
             uint32_t ch0, ch1;
             // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0) for a
@@ -1240,10 +1278,19 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 const float fy1 = __builtin_fmaf(n1.w, pa.y, __builtin_fmaf(n1.z, pc.y, -oi.y));
                 const float nz1 = __builtin_fmaf(n2.z, pa.z, __builtin_fmaf(n2.w, pc.z, -oi.z));
                 const float fz1 = __builtin_fmaf(n2.w, pa.z, __builtin_fmaf(n2.z, pc.z, -oi.z));
+#if RT_SLAB_ASM
+                // the plane distances are FMA results and t_best_c is canonical, so min/max need no
+                // canonicalising v_max (LLVM re-emits one per visit for a value carried into the loop)
+                c0min = vmax3(nx0, ny0, vmax(tmin_s, nz0));
+                c0max = vmin3(fx0, fy0, vmin(fz0, t_best_c)) * kSlabSlack;
+                c1min = vmax3(nx1, ny1, vmax(tmin_s, nz1));
+                c1max = vmin3(fx1, fy1, vmin(fz1, t_best_c)) * kSlabSlack;
+#else
                 c0min = fmaxf(fmaxf(nx0, ny0), fmaxf(nz0, kTmin));
                 c0max = fminf(fminf(fx0, fy0), fminf(fz0, t_best_c)) * kSlabSlack;
                 c1min = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, kTmin));
                 c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best_c)) * kSlabSlack;
+#endif
             };
             if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
                 const uint32_t noff = (uint32_t)node << 6;
@@ -1279,11 +1326,17 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 cnt.boxes += 2;
                 cnt.wnode += wave_leader();
                 if (__ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0) cnt.wnode_uniform += wave_leader();
+                const uint32_t act = (uint32_t)__popcll(__ballot(1));
+                if (wave_leader()) {
+                    cnt.idle_nt += 64u - ntrav;
+                    cnt.idle_fin += ntrav - n_outer;
+                    cnt.idle_wait += n_outer - act;
+                }
             }
             const bool h0 = c0min <= c0max;
             const bool h1 = c1min <= c1max;
-            const bool both = h0 && h1, none = !(h0 || h1);
             const bool swap = c1min < c0min;
+            const bool both = h0 && h1, none = !(h0 || h1);
             const uint32_t nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
             const uint32_t farc = swap ? ch0 : ch1;
             stk[sp * 64] = (int16_t)farc;
@@ -1305,22 +1358,30 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         // One primitive per lane per iteration: a lane walks its leaf's primitives and then the leaves
         // that follow on its stack with its own cursor, so lanes with short leaves do not wait for the
         // wave's longest leaf (same primitives in the same order per lane as a per-leaf loop).
+        // cursor and end in units of kPrimStep (bytes of the 32-B primitive record with RT_PRIM_BUFFER)
         uint32_t cur = 0u, end = 0u;
         if (leaf >= 0x8000u) {
             const uint32_t l = leaf ^ 0xffffu;
-            cur = l >> 2;
-            end = cur + (l & 3u) + 1u;
+            cur = (l >> 2) * kPrimStep;
+            end = cur + ((l & 3u) + 1u) * kPrimStep;
         }
         while (cur < end) {
             {
-                const uint32_t i = cur;
+                const uint32_t i = cur / kPrimStep;  // the primitive's index (a shift, needed only on a hit)
+#if RT_PRIM_BUFFER
+                // byte offsets through a buffer descriptor: no 64-bit address arithmetic per primitive, and
+                // two 16-B loads (two texture-addresser requests) per test
+                const float4 p0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, cur, 0, 0));
+                const float4 p1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, cur + 16u, 0, 0));
+#else
                 const float4 p0 = prims[2 * i + 0];
                 const float4 p1 = prims[2 * i + 1];
+#endif
                 const uint32_t type = __float_as_uint(p1.w) & 15u;
                 if (COUNT_TESTS) {
                     cnt.prims++;
                     cnt.wleaf += wave_leader();
-                    if (__ballot(i != (uint32_t)__builtin_amdgcn_readfirstlane(i)) == 0) cnt.wleaf_uniform += wave_leader();
+                    if (__ballot(cur != (uint32_t)__builtin_amdgcn_readfirstlane(cur)) == 0) cnt.wleaf_uniform += wave_leader();
                 }
                 if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
                     const f3 oc = sub(ro, xyz(p0));
@@ -1328,7 +1389,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     const float c = dot(oc, oc) - p1.x;
                     const float disc = b * b - a_dd * c;
                     if (disc > 0) {
-                        const float sq = disc >= 0x1p-96f ? sqrt_rn(disc) : sqrtf(disc);
+                        const float sq = sqrt_fast(disc);
                         float t = fast_div ? div_rn(-b - sq, a_dd, inv_a) : (-b - sq) / a_dd;
                         if (t < t_best && t > kTmin) {
                             t_best = t;
@@ -1360,13 +1421,14 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     }
                 }
             }
-            if (++cur == end) {
+            cur += kPrimStep;
+            if (cur == end) {
                 leaf = 0;
                 if (node >= 0x8000u) {
                     leaf = node;
                     const uint32_t l = leaf ^ 0xffffu;
-                    cur = l >> 2;
-                    end = cur + (l & 3u) + 1u;
+                    cur = (l >> 2) * kPrimStep;
+                    end = cur + ((l & 3u) + 1u) * kPrimStep;
                     node = ustk[(sp - 1u) * 64];
                     sp--;
                 }
@@ -1433,8 +1495,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     const uint64_t w_start = __builtin_amdgcn_s_memtime();
     while (true) {
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt, ntrav);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;

@@ -20,4 +20,6 @@ for v in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "6,8").split(",
           f"SIMD eff: node {boxes/2/(64*wn):.3f} leaf {prims/(64*wl):.3f} shade {rays/(64*ws):.3f} | "
           f"wave-iters per 64 rays: node {64*wn/rays:.1f} leaf {64*wl/rays:.1f} shade {64*ws/rays:.2f} | "
           f"wave time: trace {c[7]/max(1,c[9]):.3f} (leaf {c[10]/max(1,c[9]):.3f}) shade {c[8]/max(1,c[9]):.3f} "
-          f"cycles per 64 rays {64*c[9]/rays:.0f} | uniform wave-iters: node {c[11]/max(1,wn):.3f} leaf {c[12]/max(1,wl):.3f}", flush=True)
+          f"cycles per 64 rays {64*c[9]/rays:.0f} | uniform wave-iters: node {c[11]/max(1,wn):.3f} leaf {c[12]/max(1,wl):.3f} | "
+          f"node-iteration lanes: active {boxes/2/wn:.1f} idle: pixel-done {c[13]/max(1,wn):.1f} ray-finished {c[14]/max(1,wn):.1f} "
+          f"leaf-waiting {c[15]/max(1,wn):.1f}", flush=True)
