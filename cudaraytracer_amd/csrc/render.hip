@@ -67,10 +67,28 @@ __device__ __forceinline__ float sqrt_rn(const float x) {
 }
 // sqrtf(x) bit for bit: sqrt_rn in its range, LLVM's full sequence (a branch no lane usually takes) below it
 __device__ __forceinline__ float sqrt_fast(const float x) { return x >= 0x1p-96f ? sqrt_rn(x) : sqrtf(x); }
+// RN(1/a) for |a| in [2^-40, 2^40]: v_rcp_f32 and one FMA Newton step — equal to the IEEE division for every
+// binary32 in that range, both signs (tools/check_rcp.hip, exhaustive on MI355X) — 12 issue cycles instead of
+// the ~36-cycle division sequence.  rcp_ieee keeps the IEEE division outside the range (a branch no lane
+// usually takes).
+__device__ __forceinline__ bool in_rcp_range(const float a) {
+    const float m = fabsf(a);
+    return m >= 0x1p-40f && m <= 0x1p40f;
+}
+__device__ __forceinline__ float rcp_rn(const float a) {
+    const float y = __builtin_amdgcn_rcpf(a);
+    return __builtin_fmaf(__builtin_fmaf(-a, y, 1.0f), y, y);
+}
+__device__ __forceinline__ float rcp_ieee(const float a) {
+    float r;
+    if (in_rcp_range(a)) r = rcp_rn(a);
+    else r = 1.0f / a;
+    return r;
+}
 __device__ __forceinline__ float length(f3 v) { return sqrt_fast(v.x * v.x + v.y * v.y + v.z * v.z); }
 __device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, length(v)); }
 __device__ __forceinline__ f3 normalize(f3 v) {
-    float inv = 1.0f / sqrt_fast(dot(v, v));
+    float inv = rcp_ieee(sqrt_fast(dot(v, v)));
     return scale(inv, v);
 }
 // x / a correctly rounded from y = RN(1/a) (a one-off IEEE division) in five 2-cycle ops instead of the
@@ -96,7 +114,7 @@ __device__ __forceinline__ f3 divs_rn(const f3 v, const float s, const float y) 
     return divs(v, s);
 }
 __device__ __forceinline__ float recip_in_range(const float s) {
-    return fabsf(s) >= 0x1p-40f && fabsf(s) <= 0x1p40f ? 1.0f / s : 0.0f;
+    return in_rcp_range(s) ? rcp_rn(s) : 0.0f;
 }
 __device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }
 __device__ __forceinline__ float clampf(float x, float a, float b) { return (x < a) ? a : ((x > b) ? b : x); }
@@ -347,7 +365,7 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
             } else {  // XY/XZ/YZRect::Hit (Hittable.cuh:140-169, 196-225, 252-281)
                 const float ok = type == RT_XYRECT ? o.z : (type == RT_XZRECT ? o.y : o.x);
                 const float dk = type == RT_XYRECT ? d.z : (type == RT_XZRECT ? d.y : d.x);
-                const float t = (p0.x - ok) * (1.0f / dk);
+                const float t = (p0.x - ok) * rcp_ieee(dk);
                 if (!(t < kTmin || t > t_best)) {
                     const float oa = type == RT_YZRECT ? o.y : o.x, da = type == RT_YZRECT ? d.y : d.x;
                     const float ob = type == RT_XYRECT ? o.y : o.z, db = type == RT_XYRECT ? d.y : d.z;
@@ -492,7 +510,12 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
     if (hit >= 0) mtype = __float_as_uint(P->mats[3 * (hit_tag >> 4)].x) & 15u;
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
     if (hit < 0) {  // sky (Kernel.cu:41-44)
-        const float tt = 0.5f * (rd.y / length(rd) + 1.0f);
+        // rd.y / |rd|: below |rd.y| = 2^-100 the quotient's exact bits vanish in the + 1 (|q| < 2^-60)
+        const float len = length(rd);
+        float q;
+        if (in_rcp_range(len)) q = div_rn(rd.y, len, rcp_rn(len));
+        else q = rd.y / len;
+        const float tt = 0.5f * (q + 1.0f);
         const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
         contrib = mulv(att, c);
         return SHADE_ENDED;
@@ -538,11 +561,12 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         contrib = mulv(e, att);
         return SHADE_ENDED;
     }
-    float len = 1.0f;
+    float len = 1.0f, y_len = 0.0f;
     f3 ud = mk(0.0f, 0.0f, 0.0f);
     if (specular) {
         len = length(rd);
-        ud = divs_rn(rd, len, recip_in_range(len));
+        y_len = recip_in_range(len);
+        ud = divs_rn(rd, len, y_len);
     }
     if (mtype == RT_DIELECTRIC) {  // Dielectric::Scatter (Material.cuh:106-136); attenuation (1,1,1)
         // Evaluated in an order that keeps few values live: every quantity is the same binary32 value the
@@ -552,7 +576,10 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         const float4 m1 = P->mats[3 * mat + 1];
         const float dn = dot(rd, normal);
         const bool exiting = dn > 0.0f;
-        float cosine = (exiting ? dn : -dn) / len;
+        const float cn = exiting ? dn : -dn;
+        float cosine;
+        if (y_len != 0.0f && fabsf(cn) >= 0x1p-100f) cosine = div_rn(cn, len, y_len);
+        else cosine = cn / len;
         if (exiting) cosine = sqrtf(1.0f - ir * ir * (1 - cosine * cosine));
         const float ni_over_nt = exiting ? ir : m1.x;
         const f3 outward_normal = exiting ? neg(normal) : normal;
@@ -1022,7 +1049,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
                         } else {  // *Rect::Hit
                             const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
                             const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
-                            const float t = (p0.x - ok) * (1.0f / dk);
+                            const float t = (p0.x - ok) * rcp_ieee(dk);
                             if (!(t < kTmin || t > t_best)) {
                                 const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
                                 const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
@@ -1208,6 +1235,12 @@ __device__ __forceinline__ float vmin3(float a, float b, float c) { float r; asm
 #define RT_PRIM_BUFFER 1
 #endif
 constexpr uint32_t kPrimStep = RT_PRIM_BUFFER ? 32u : 1u;
+#ifndef RT_V3_NODES64
+#define RT_V3_NODES64 0
+#endif
+#ifndef RT_SCALAR_NODES64
+#define RT_SCALAR_NODES64 0
+#endif
 #ifndef RT_SCALAR_NODES
 #define RT_SCALAR_NODES 1
 #endif
@@ -1218,7 +1251,7 @@ constexpr bool kScalarNodes = RT_SCALAR_NODES != 0;
 // still tracing (the wave then shades the finished lanes and regenerates them).
 template <bool COUNT_TESTS, int NODES>
 __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, const __amdgpu_buffer_rsrc_t rrsrc,
-                                            const float4* __restrict__ nodes48, const uint32_t* __restrict__ refs16,
+                                            const float4* __restrict__ nodes_tab, const uint32_t* __restrict__ refs16,
                                             const float4* __restrict__ prims, int16_t* const stk,
                                             const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
                                             Counts& cnt, const uint32_t ntrav = 64) {
@@ -1231,8 +1264,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     float t_best = c.t_best;
     const float a_dd = dot(rd, rd);
     // RN(1/a) for the sphere roots (div_rn); outside [2^-40, 2^40] the test divides the IEEE way
-    const float inv_a = 1.0f / a_dd;
     const bool fast_div = a_dd >= 0x1p-40f && a_dd <= 0x1p40f;
+    const float inv_a = rcp_rn(a_dd);  // used only when fast_div
     const f3 invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
                        fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
@@ -1292,20 +1325,29 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best_c)) * kSlabSlack;
 #endif
             };
-            if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
-                const uint32_t noff = (uint32_t)node << 6;
-                const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
-                ch0 = r2.x & 0xffffu;
-                ch1 = r2.y & 0xffffu;
-                slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
-                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
-                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
+            if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references (one offset)
+                const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
+                if (RT_SCALAR_NODES64 && __ballot(node != nu) == 0) {  // wave-uniform node: one scalar load
+                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes_tab + nu * 64u);
+                    ch0 = __float_as_uint(cn[12]) & 0xffffu;
+                    ch1 = __float_as_uint(cn[13]) & 0xffffu;
+                    slab(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
+                         make_float4(cn[8], cn[9], cn[10], cn[11]));
+                } else {
+                    const uint32_t noff = (uint32_t)node << 6;
+                    const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
+                    ch0 = r2.x & 0xffffu;
+                    ch1 = r2.y & 0xffffu;
+                    slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
+                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
+                }
             } else {  // 48 B of f32 boxes + 4 B of references
                 const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
                 if (kScalarNodes && __ballot(node != nu) == 0) {
                     // every active lane visits the same node: scalar loads through the constant cache, planes as
                     // SGPR operands of the FMAs — no vector-memory (TA/TD) traffic, the kernel's busiest unit
-                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes48 + nu * 48u);
+                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes_tab + nu * 48u);
                     const uint32_t refs = *(const ConstU32*)((const ConstU8*)refs16 + nu * 4u);
                     ch0 = refs & 0xffffu;
                     ch1 = refs >> 16;
@@ -1407,7 +1449,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 } else {  // *Rect::Hit
                     const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
                     const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
-                    const float t = (p0.x - ok) * (1.0f / dk);
+                    const float t = (p0.x - ok) * rcp_ieee(dk);
                     if (!(t < kTmin || t > t_best)) {
                         const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
                         const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
@@ -1451,7 +1493,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
 template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false, bool COMPACT = false>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
-    constexpr int NODES = NODES_48;
+    constexpr int NODES = RT_V3_NODES64 ? NODES_64 : NODES_48;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t* const wl = (uint32_t*)lds;
@@ -1497,7 +1539,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt, ntrav);
+            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt, ntrav);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -1600,7 +1642,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     const uint32_t threshold = P.regen_threshold;
 
     while (true) {
-        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
         uint32_t sample, depth, rays;
