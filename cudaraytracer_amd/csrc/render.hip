@@ -1235,12 +1235,6 @@ __device__ __forceinline__ float vmin3(float a, float b, float c) { float r; asm
 #define RT_PRIM_BUFFER 1
 #endif
 constexpr uint32_t kPrimStep = RT_PRIM_BUFFER ? 32u : 1u;
-#ifndef RT_V3_NODES64
-#define RT_V3_NODES64 0
-#endif
-#ifndef RT_SCALAR_NODES64
-#define RT_SCALAR_NODES64 0
-#endif
 #ifndef RT_SCALAR_NODES
 #define RT_SCALAR_NODES 1
 #endif
@@ -1325,23 +1319,14 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best_c)) * kSlabSlack;
 #endif
             };
-            if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references (one offset)
-                const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
-                if (RT_SCALAR_NODES64 && __ballot(node != nu) == 0) {  // wave-uniform node: one scalar load
-                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes_tab + nu * 64u);
-                    ch0 = __float_as_uint(cn[12]) & 0xffffu;
-                    ch1 = __float_as_uint(cn[13]) & 0xffffu;
-                    slab(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
-                         make_float4(cn[8], cn[9], cn[10], cn[11]));
-                } else {
-                    const uint32_t noff = (uint32_t)node << 6;
-                    const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
-                    ch0 = r2.x & 0xffffu;
-                    ch1 = r2.y & 0xffffu;
-                    slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
-                }
+            if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
+                const uint32_t noff = (uint32_t)node << 6;
+                const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
+                ch0 = r2.x & 0xffffu;
+                ch1 = r2.y & 0xffffu;
+                slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
+                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
+                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
             } else {  // 48 B of f32 boxes + 4 B of references
                 const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
                 if (kScalarNodes && __ballot(node != nu) == 0) {
@@ -1493,7 +1478,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
 template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false, bool COMPACT = false>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
-    constexpr int NODES = RT_V3_NODES64 ? NODES_64 : NODES_48;
+    constexpr int NODES = NODES_48;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t* const wl = (uint32_t*)lds;
