@@ -38,28 +38,57 @@ def local_row_counts(height: int, band_rows: int, world: int) -> list[int]:
     return [len(band_rows_of(height, band_rows, world, r)) for r in range(world)]
 
 
-@functools.lru_cache(maxsize=64)
-def _rows_index(height: int, band_rows: int, world: int, rank: int, device: str) -> torch.Tensor:
-    return torch.tensor(band_rows_of(height, band_rows, world, rank), dtype=torch.long, device=device)
+_BUFFERS: dict = {}
+
+
+def _buffers(key, world: int, rank: int, dst: int, max_rows: int, width: int, height: int, dtype, dev):
+    """Send / receive / frame buffers of one gather shape, allocated once (the bench gathers every step)."""
+    b = _BUFFERS.get(key)
+    if b is None:
+        if len(_BUFFERS) > 16:
+            _BUFFERS.clear()
+        send = torch.zeros(max_rows * width, dtype=dtype, device=dev)
+        recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+        full = torch.empty(height, width, dtype=dtype, device=dev) if rank == dst else None
+        b = _BUFFERS[key] = (send, recv, full)
+    return b
+
+
+def unshuffle_into(full: torch.Tensor, recv: list, height: int, width: int, band_rows: int) -> None:
+    """Rank r's local rows are the bands r, r + N, r + 2N, ... of the frame: every complete round of N bands
+    is one strided copy per rank, the ragged last round one small copy per rank."""
+    world = len(recv)
+    rnd = band_rows * world
+    k = height // rnd
+    if k:
+        full4 = full[: k * rnd].view(k, world, band_rows, width)
+        for r in range(world):
+            full4[:, r].copy_(recv[r][: k * band_rows * width].view(k, band_rows, width))
+    base = k * band_rows * width
+    for r in range(world):
+        start = k * rnd + r * band_rows
+        if start >= height:
+            break
+        n = min(band_rows, height - start)
+        full[start:start + n].copy_(recv[r][base: base + n * width].view(n, width))
 
 
 def gather_bands(local: torch.Tensor, width: int, height: int, band_rows: int, dst: int = 0,
                  group=None) -> torch.Tensor | None:
-    """Gather every rank's (local_rows·W) framebuffer to `dst` and return the (H, W) image there.  With
-    the gloo backend (CPU tests, single-GPU rehearsals) device buffers are staged through host memory."""
+    """Gather every rank's (local_rows·W) framebuffer to `dst` and return the (H, W) image there (a buffer
+    reused by later calls of the same shape).  With the gloo backend (CPU tests, single-GPU rehearsals)
+    device buffers are staged through host memory."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     counts = local_row_counts(height, band_rows, world)
     max_rows = max(counts)
     via_host = local.is_cuda and dist.get_backend(group) == "gloo"
     dev = torch.device("cpu") if via_host else local.device
-    send = torch.zeros(max_rows * width, dtype=local.dtype, device=dev)
-    send[: local.numel()] = local.reshape(-1).to(dev)
-    recv = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    key = (id(group), world, rank, dst, max_rows, width, height, band_rows, local.dtype, str(dev))
+    send, recv, full = _buffers(key, world, rank, dst, max_rows, width, height, local.dtype, dev)
+    send[: local.numel()].copy_(local.reshape(-1))
     dist.gather(send, recv, dst=dst, group=group)
     if rank != dst:
         return None
-    full = torch.empty(height, width, dtype=local.dtype, device=dev)
-    for r in range(world):
-        full.index_copy_(0, _rows_index(height, band_rows, world, r, str(dev)), recv[r][: counts[r] * width].view(counts[r], width))
+    unshuffle_into(full, recv, height, width, band_rows)
     return full.to(local.device) if via_host else full

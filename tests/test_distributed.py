@@ -65,3 +65,26 @@ def test_band_rows_partition_the_image():
     for h, b, n in [(1080, 16, 8), (37, 16, 3), (4320, 16, 8), (7, 16, 4)]:
         rows = sorted(r for k in range(n) for r in band_rows_of(h, b, n, k))
         assert rows == list(range(h))
+
+
+@pytest.mark.parametrize("height, band_rows, world", [(72, 16, 2), (72, 5, 3), (37, 16, 8), (128, 16, 8), (4320, 16, 8),
+                                                      (17, 4, 1), (3, 16, 4)])
+def test_unshuffle_matches_row_index_reassembly(height, band_rows, world):
+    """The strided unshuffle puts every rank's local rows at the global rows band_rows_of assigns them."""
+    sys.path.insert(0, ROOT)
+    from cudaraytracer_amd import parallel
+    from cudaraytracer_amd.renderer import band_rows_of
+
+    width = 7
+    frame = torch.arange(height * width, dtype=torch.int64).view(height, width)
+    counts = [len(band_rows_of(height, band_rows, world, r)) for r in range(world)]
+    recv = []
+    for r in range(world):
+        rows = band_rows_of(height, band_rows, world, r)
+        buf = torch.full((max(counts) * width,), -1, dtype=torch.int64)
+        if rows:
+            buf[: len(rows) * width] = frame[rows].reshape(-1)
+        recv.append(buf)
+    full = torch.full((height, width), -2, dtype=torch.int64)
+    parallel.unshuffle_into(full, recv, height, width, band_rows)
+    assert torch.equal(full, frame)
