@@ -272,7 +272,8 @@ def main() -> None:
                 "workload": (f"{args.config}: {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}, "
                              f"{scenes.CONFIGS[args.config].description.split(', ', 3)[-1]}"),
                 "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
-                "parallelism": f"{world} rank(s) x 16-row bands + RCCL gather" if world > 1 else "1 GPU",
+                "parallelism": (f"{world} rank(s) x 16-row bands + {'RCCL' if args.backend == 'nccl' else args.backend} gather"
+                                if world > 1 else "1 GPU"),
                 "kernel_variant": args.variant,
             },
             "kernel_ms": round(kernel_ms, 3),
