@@ -89,10 +89,11 @@ def cpu_baseline(cfg: scenes.Config, target_s: float) -> dict:
                       f"{dt1:.2f} s"}
 
 
-def philox_mode(cfg: scenes.Config, scene: DeviceScene, inputs, steps: int) -> dict:
+def secondary_mode(cfg: scenes.Config, scene: DeviceScene, inputs, steps: int, rng: str = "philox",
+                   state_layout: str = "curand") -> dict:
     """Secondary figure: the same frames with the stateless Philox RNG (RT_FLAG_RNG_PHILOX, no per-pixel
-    RNG state in HBM).  Not the headline: the reference's stream is XORWOW."""
-    r = Renderer(cfg.width, cfg.height, rng="philox")
+    RNG state in HBM), or with the other XORWOW state layout."""
+    r = Renderer(cfg.width, cfg.height, rng=rng, state_layout=state_layout)
     r.render_init()
     r.render(scene, cfg.spp, cfg.depth, inputs)  # warm-up
     torch.cuda.synchronize()
@@ -105,11 +106,12 @@ def philox_mode(cfg: scenes.Config, scene: DeviceScene, inputs, steps: int) -> d
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     rays = int(r.counters[0]) / steps
+    state_bytes = 0 if rng == "philox" else (48 if state_layout == "curand" else 24) * cfg.width * cfg.height
     return {"value": round(rays / ms / 1e3, 2), "unit": "Mray/s", "kernel_ms": round(ms, 3),
-            "rays_per_frame": int(rays), "hbm_rng_state_bytes": 0}
+            "rays_per_frame": int(rays), "hbm_rng_state_bytes": state_bytes}
 
 
-def pmc_profile(config: str, rng: str) -> dict:
+def pmc_profile(config: str, rng: str, state_layout: str = "curand") -> dict:
     """HBM bytes per launch and SIMD-efficiency counters of the default kernel from the committed rocprofv3
     PMC summary (profiles/pmc_<config>_n1.json, tools/profile_pmc.sh), or {}.  Under weak scaling every
     rank launches the same 1920x1080-sized share, so the N=1 per-launch figures apply per rank."""
@@ -118,7 +120,7 @@ def pmc_profile(config: str, rng: str) -> dict:
         return {}
     with open(path) as f:
         d = json.load(f)
-    d = d.get("philox", {}) if rng == "philox" else d
+    d = d.get("philox", {}) if rng == "philox" else (d.get("soa", {}) if state_layout == "soa" else d)
     keys = ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch", "valu_lane_utilization", "avg_waves_per_simd",
             "ta_busy_frac_per_cu", "kernel")
     return {k: d[k] for k in keys if k in d}
@@ -166,6 +168,9 @@ def main() -> None:
     ap.add_argument("--rng", choices=("xorwow", "philox"), default="xorwow",
                     help="xorwow: the reference's per-pixel cuRAND state (parity mode, headline); philox: stateless "
                          "Philox4x32-10 streams (RT_FLAG_RNG_PHILOX)")
+    ap.add_argument("--state-layout", choices=("soa", "curand"), default="soa",
+                    help="XORWOW states: soa = native six uint32 planes (RT_FLAG_STATE_SOA, 24 B/pixel, the same "
+                         "streams); curand = the reference's 48-B curandState structs (the LaunchKernel layout)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-philox-line", action="store_true", help="skip the secondary Philox-mode timing (N=1)")
@@ -197,7 +202,8 @@ def main() -> None:
     lib().rt_set_variant(args.variant)
 
     band = parallel.DEFAULT_BAND_ROWS if world > 1 else cfg.height
-    r = Renderer(cfg.width, cfg.height, device=device, band_rows=band, num_ranks=world, rank=rank, rng=args.rng)
+    r = Renderer(cfg.width, cfg.height, device=device, band_rows=band, num_ranks=world, rank=rank, rng=args.rng,
+                 state_layout=args.state_layout)
     scene = DeviceScene(scenes.builtin(cfg.scene))
     inputs = cfg.inputs()
     r.render_init()
@@ -250,7 +256,7 @@ def main() -> None:
 
     if rank == 0:
         achieved = f_launch / (kernel_ms * 1e-3) / 1e12
-        pmc = pmc_profile(args.config, args.rng) if args.config == "c2" and world == 1 else {}
+        pmc = pmc_profile(args.config, args.rng, args.state_layout) if args.config == "c2" and world == 1 else {}
         rays_per_launch = c[0]
         metric = ("Mray/s (and ms/frame) at 1920x1080, 64 spp, depth 8, random-spheres" if not strong else
                   "Mray/s (and ms/frame) at 7680x4320, 128 spp, depth 8, random-spheres (8-GPU tile-split config)")
@@ -267,6 +273,7 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "f32",
             "rng": args.rng,
+            "state_layout": args.state_layout if args.rng == "xorwow" else None,
             "data": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
             "config": {
                 "workload": (f"{args.config}: {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}, "
@@ -302,7 +309,11 @@ def main() -> None:
             },
         }
         if world == 1 and args.rng == "xorwow" and not args.no_philox_line and not strong:
-            line["philox_mode"] = philox_mode(cfg, scene, inputs, args.steps)
+            line["philox_mode"] = secondary_mode(cfg, scene, inputs, args.steps)
+            other = "curand" if args.state_layout == "soa" else "soa"
+            line[f"{other}_state_layout"] = dict(secondary_mode(cfg, scene, inputs, args.steps, "xorwow", other),
+                                                 hbm_bytes_per_launch=pmc_profile(args.config, "xorwow", other).get(
+                                                     "hbm_bytes_per_launch"))
         if world == 1 and not args.no_cpu_baseline and not strong:
             line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         print(json.dumps(line), flush=True)

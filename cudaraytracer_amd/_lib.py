@@ -27,6 +27,8 @@ EXPORTED = [
     "rt_scene_destroy",
     "rt_scene_get_info",
     "rt_render_init",
+    "rt_render_init_soa",
+    "rt_soa_plane_words",
     "rt_render",
     "rt_tiled_create",
     "rt_tiled_render",
@@ -71,6 +73,9 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_scene_destroy.argtypes = [vp]
     lib.rt_scene_get_info.argtypes = [vp, P(abi.SceneInfo)]
     lib.rt_render_init.argtypes = [vp, C.c_uint32, C.c_uint32, P(abi.Tiling), C.c_uint64, vp]
+    lib.rt_render_init_soa.argtypes = [vp, C.c_uint32, C.c_uint32, P(abi.Tiling), C.c_uint64, vp]
+    lib.rt_soa_plane_words.argtypes = [C.c_uint32, C.c_uint32]
+    lib.rt_soa_plane_words.restype = C.c_uint64
     lib.rt_render.argtypes = [vp, P(abi.RenderArgs), vp]
     lib.rt_set_timing.argtypes = [C.c_int]
     lib.rt_tiled_create.argtypes = [P(abi.TiledDesc), P(abi.SceneDesc), P(vp)]

@@ -20,6 +20,7 @@ RT_FLAG_ACCUMULATE = 1 << 2
 RT_FLAG_RIUS_LEFT_TO_RIGHT = 1 << 3
 RT_FLAG_COUNT_TESTS = 1 << 4
 RT_FLAG_RNG_PHILOX = 1 << 5
+RT_FLAG_STATE_SOA = 1 << 6
 
 STATUS = {
     0: "RT_OK",

@@ -208,7 +208,8 @@ struct KParams {
     uint32_t* pos;
     float4* radiance;
     float4* accum;
-    uint32_t* state;  // 12 words per rt_curand_state
+    uint32_t* state;  // XORWOW states: 12-word rt_curand_state per pixel, or (RT_FLAG_STATE_SOA) six planes
+    uint32_t state_stride;  // distance between a pixel's state words: 1 (rt_curand_state) or the plane size
     unsigned long long* counters;
     uint32_t num_nodes, num_prims;
     uint32_t width, height, spp, max_depth, flags;
@@ -634,8 +635,18 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
 // Pixel epilogue (Kernel.cu:149-157): RNG state store, average, gamma 2, RGBA8 pack; optional outputs.
 __device__ __forceinline__ void store_rng(const KParams& P, uint32_t* st, const Rng& rng) {
     if (!(P.flags & RT_FLAG_NO_STATE_WRITEBACK)) {
-        *reinterpret_cast<uint4*>(st) = make_uint4(rng.d, rng.v0, rng.v1, rng.v2);
-        *reinterpret_cast<uint2*>(st + 4) = make_uint2(rng.v3, rng.v4);
+        const uint32_t k = P.state_stride;
+        if (k == 1u) {  // the reference's 48-B curandState: d, v[5] are its first 24 bytes
+            *reinterpret_cast<uint4*>(st) = make_uint4(rng.d, rng.v0, rng.v1, rng.v2);
+            *reinterpret_cast<uint2*>(st + 4) = make_uint2(rng.v3, rng.v4);
+        } else {  // six planes: each word a coalesced 4-B access of the wave
+            st[0] = rng.d;
+            st[k] = rng.v0;
+            st[2 * k] = rng.v1;
+            st[3 * k] = rng.v2;
+            st[4 * k] = rng.v3;
+            st[5 * k] = rng.v4;
+        }
     }
 }
 
@@ -738,10 +749,24 @@ __device__ __forceinline__ KParamsC* kparams_reload() {
     return p;
 }
 
-__device__ __forceinline__ Rng load_rng(const uint32_t* st) {
-    const uint4 s03 = *reinterpret_cast<const uint4*>(st);
-    const uint2 s45 = *reinterpret_cast<const uint2*>(st + 4);
-    return Rng{s03.x, s03.y, s03.z, s03.w, s45.x, s45.y};
+// The pixel's first state word; its words are P.state_stride apart (1: rt_curand_state; the plane size with
+// RT_FLAG_STATE_SOA, whose planes hold the pixels 8×8 tile by tile — tile t, row r, column c at t·64 + 8r + c
+// — so the wave that renders a tile reads and writes 256 contiguous bytes per plane).
+__device__ __forceinline__ uint32_t soa_index(uint32_t x, uint32_t ly, uint32_t width) {
+    return ((((ly >> 3) * ((width + 7u) >> 3)) + (x >> 3)) << 6) + ((ly & 7u) << 3) + (x & 7u);
+}
+__device__ __forceinline__ uint32_t* state_at(const KParams& P, size_t pix) {
+    if (P.state_stride == 1u) return P.state + pix * 12;
+    const uint32_t ly = (uint32_t)(pix / P.width), x = (uint32_t)(pix - (size_t)ly * P.width);  // once per pixel
+    return P.state + soa_index(x, ly, P.width);
+}
+__device__ __forceinline__ Rng load_rng(const uint32_t* st, uint32_t k) {
+    if (k == 1u) {
+        const uint4 s03 = *reinterpret_cast<const uint4*>(st);
+        const uint2 s45 = *reinterpret_cast<const uint2*>(st + 4);
+        return Rng{s03.x, s03.y, s03.z, s03.w, s45.x, s45.y};
+    }
+    return Rng{st[0], st[k], st[2 * k], st[3 * k], st[4 * k], st[5 * k]};
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -829,9 +854,11 @@ __device__ __forceinline__ void draw3(RngPhilox& s, float& a, float& b, float& c
 __device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPhilox&) {}  // stateless in HBM
 
 // Start of a pixel's frame: its XORWOW state from HBM, or its Philox stream at draw 0.
-template <class R> __device__ __forceinline__ R begin_rng(const uint32_t* st, uint32_t pixel);
-template <> __device__ __forceinline__ Rng begin_rng<Rng>(const uint32_t* st, uint32_t) { return load_rng(st); }
-template <> __device__ __forceinline__ RngPhilox begin_rng<RngPhilox>(const uint32_t*, uint32_t pixel) {
+template <class R> __device__ __forceinline__ R begin_rng(const uint32_t* st, uint32_t stride, uint32_t pixel);
+template <> __device__ __forceinline__ Rng begin_rng<Rng>(const uint32_t* st, uint32_t stride, uint32_t) {
+    return load_rng(st, stride);
+}
+template <> __device__ __forceinline__ RngPhilox begin_rng<RngPhilox>(const uint32_t*, uint32_t, uint32_t pixel) {
     KParamsC* q = kparams_reload();
     return RngPhilox{0u, 0u, 0u, 0u, 0u, pixel, q->rng_key_lo, q->rng_key_hi, q->rng_frame};
 }
@@ -846,8 +873,8 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
     uint32_t x, g;
     size_t pix;
     if (!lane_pixel(P, x, g, pix)) return;
-    uint32_t* st = P.state + pix * 12;
-    Rng rng = load_rng(st);
+    uint32_t* st = state_at(P, pix);
+    Rng rng = load_rng(st, P.state_stride);
     const Camera cam = lane_camera(&P, x, g);
     const bool rtl = P.rius_rtl != 0;
 
@@ -913,8 +940,8 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
     uint32_t x, g;
     size_t pix;
     if (!lane_pixel<BLOCK>(P, x, g, pix)) return;
-    uint32_t* st = P.state + pix * 12;
-    Rng rng = load_rng(st);
+    uint32_t* st = state_at(P, pix);
+    Rng rng = load_rng(st, P.state_stride);
     const Camera cam = lane_camera(&P, x, g);
     const bool rtl = P.rius_rtl != 0;
 
@@ -1506,8 +1533,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     Cursor c{kSentinel16, 0, -1, 0u, 0u, FLT_MAX, MODE_DONE};
 
     {  // first camera ray of the pixel
-        uint32_t* st = P.state + pix * 12;
-        R rng = begin_rng<R>(st, g * P.width + x);  // global pixel index (Kernel.cu:119)
+        uint32_t* st = state_at(P, pix);
+        R rng = begin_rng<R>(st, P.state_stride, g * P.width + x);  // global pixel index (Kernel.cu:119)
         f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
         // (sample = -1: v3_next_sample starts sample 0; with spp = 0 it stays 0, so compact parking's packed
         // sample field cannot spill into the ray count)
@@ -1565,7 +1592,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
     cnt.rays = rays;
     cnt.primary = P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
-    finish_pixel<COUNT_TESTS>(P, pix, P.state + pix * 12, rng, col, cnt);
+    finish_pixel<COUNT_TESTS>(P, pix, state_at(P, pix), rng, col, cnt);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1648,7 +1675,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                     cam = true;
                 } else {  // the pixel is done (Kernel.cu:149-157)
                     const uint32_t pix = park[PK_PIX * 64];
-                    write_pixel(P, pix, P.state + (size_t)pix * 12, rng, col);
+                    write_pixel(P, pix, state_at(P, pix), rng, col);
                     fin = true;
                 }
             } else {
@@ -1683,7 +1710,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                         park[PK_X * 64] = x;
                         park[PK_G * 64] = g;
                         park[PK_PIX * 64] = pix;
-                        rng = begin_rng<R>(P.state + (size_t)pix * 12, g * P.width + x);
+                        rng = begin_rng<R>(state_at(P, pix), P.state_stride, g * P.width + x);
                         col = mk(0.0f, 0.0f, 0.0f);
                         sample = 0u;
                         cam = true;
@@ -1715,11 +1742,20 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
 }
 
 // RenderInit (Kernel.cu:166-176): curand_init(seed_base + global_pixel_index, 0, 0).
-__device__ __forceinline__ void curand_init_state(unsigned long long seed, uint32_t* st) {
+__device__ __forceinline__ void curand_init_state(unsigned long long seed, uint32_t* st, uint32_t k = 1u) {
     const uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
     const uint32_t s1 = ((uint32_t)(seed >> 32)) ^ 0xf7dcefddu;
     const uint32_t t0 = 1099087573u * s0;
     const uint32_t t1 = 2591861531u * s1;
+    if (k != 1u) {  // RT_FLAG_STATE_SOA: d, v[5] only, one plane each
+        st[0] = 6615241u + t1 + t0;
+        st[k] = 123456789u + t0;
+        st[2 * k] = 362436069u ^ t0;
+        st[3 * k] = 521288629u + t1;
+        st[4 * k] = 88675123u ^ t1;
+        st[5 * k] = 5783321u + t0;
+        return;
+    }
     *reinterpret_cast<uint4*>(st) = make_uint4(6615241u + t1 + t0, 123456789u + t0, 362436069u ^ t0, 521288629u + t1);
     *reinterpret_cast<uint4*>(st + 4) = make_uint4(88675123u ^ t1, 5783321u + t0, 0u, 0u);
     *reinterpret_cast<uint4*>(st + 8) = make_uint4(0u, 0u, 0u, 0u);  // boxmuller_extra, pad, extra_double
@@ -1727,14 +1763,16 @@ __device__ __forceinline__ void curand_init_state(unsigned long long seed, uint3
 
 __global__ __launch_bounds__(kBlock) void render_init_kernel(uint32_t* state, uint32_t width, uint32_t local_rows,
                                                               uint32_t band_rows, uint32_t num_ranks, uint32_t rank,
-                                                              unsigned long long seed_base) {
+                                                              unsigned long long seed_base, uint32_t soa) {  // soa: plane size
     const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= (size_t)width * local_rows) return;
+    const size_t n = (size_t)width * local_rows;
+    if (i >= n) return;
     const uint32_t ly = (uint32_t)(i / width), x = (uint32_t)(i - (size_t)ly * width);
     const uint32_t band = ly / band_rows, within = ly - band * band_rows;
     const uint32_t g = (band * num_ranks + rank) * band_rows + within;
     const uint32_t pixel_index = g * width + x;  // unsigned, as Kernel.cu:174
-    curand_init_state(seed_base + pixel_index, state + i * 12);
+    if (soa) curand_init_state(seed_base + pixel_index, state + soa_index(x, ly, width), soa);
+    else curand_init_state(seed_base + pixel_index, state + i * 12);
 }
 
 // LaunchRenderInit's kernel honours the caller's grid/block exactly (Kernel.cu:166-176).
@@ -2098,6 +2136,16 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.radiance = (float4*)a->radiance;
     P.accum = (float4*)a->accum;
     P.state = (uint32_t*)a->state;
+    if (a->flags & RT_FLAG_STATE_SOA) {  // six planes of whole 8×8 tiles
+        const uint64_t plane = rt_soa_plane_words(a->width, T.local_rows);
+        if (plane > 0xffffffffull) {
+            set_error("rt_render: RT_FLAG_STATE_SOA needs < 2^32 pixels per rank");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        P.state_stride = (uint32_t)plane;
+    } else {
+        P.state_stride = 1u;
+    }
     P.counters = (unsigned long long*)a->counters;
     P.num_nodes = S.num_nodes;
     P.num_prims = S.num_prims;
@@ -2269,23 +2317,47 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     return rc;
 }
 
-int rt_render_init(rt_curand_state* d_state, uint32_t width, uint32_t height, const rt_tiling* tiling,
-                   uint64_t seed_base, rt_stream stream) {
-    if (!tiling) { set_error("rt_render_init: NULL tiling"); return RT_ERR_INVALID_ARGUMENT; }
+uint64_t rt_soa_plane_words(uint32_t width, uint32_t local_rows) {
+    return (((uint64_t)width + 7u) / 8u) * (((uint64_t)local_rows + 7u) / 8u) * 64u;
+}
+
+namespace {
+int render_init(void* d_state, uint32_t width, const rt_tiling* tiling, uint64_t seed_base, rt_stream stream,
+                uint32_t soa, const char* who) {  // soa: 0 = rt_curand_state, else the plane layout
+    if (!tiling) { set_error(std::string(who) + ": NULL tiling"); return RT_ERR_INVALID_ARGUMENT; }
     if ((size_t)width * tiling->local_rows == 0) return RT_OK;  // nothing to seed
-    if (!d_state) { set_error("rt_render_init: NULL state"); return RT_ERR_INVALID_ARGUMENT; }
+    if (!d_state) { set_error(std::string(who) + ": NULL state"); return RT_ERR_INVALID_ARGUMENT; }
     if (tiling->band_rows == 0 || tiling->num_ranks == 0 || tiling->rank >= tiling->num_ranks) {
-        set_error("rt_render_init: invalid tiling");
+        set_error(std::string(who) + ": invalid tiling");
         return RT_ERR_INVALID_ARGUMENT;
     }
-    (void)height;
     const size_t n = (size_t)width * tiling->local_rows;
-    if (n == 0) return RT_OK;
+    if (soa) {
+        const uint64_t plane = rt_soa_plane_words(width, tiling->local_rows);
+        if (plane > 0xffffffffull) {
+            set_error(std::string(who) + ": needs < 2^32 pixels per rank");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        soa = (uint32_t)plane;  // the kernel's plane stride
+    }
     (void)hipGetLastError();
     hipLaunchKernelGGL(dev::render_init_kernel, dim3((unsigned)((n + dev::kBlock - 1) / dev::kBlock)), dim3(dev::kBlock), 0,
                        (hipStream_t)stream, (uint32_t*)d_state, width, tiling->local_rows, tiling->band_rows,
-                       tiling->num_ranks, tiling->rank, (unsigned long long)seed_base);
-    return hip_check(hipGetLastError(), "rt_render_init: kernel launch", RT_ERR_LAUNCH);
+                       tiling->num_ranks, tiling->rank, (unsigned long long)seed_base, soa);
+    return hip_check(hipGetLastError(), (std::string(who) + ": kernel launch").c_str(), RT_ERR_LAUNCH);
+}
+}  // namespace
+
+int rt_render_init(rt_curand_state* d_state, uint32_t width, uint32_t height, const rt_tiling* tiling,
+                   uint64_t seed_base, rt_stream stream) {
+    (void)height;
+    return render_init(d_state, width, tiling, seed_base, stream, 0u, "rt_render_init");
+}
+
+int rt_render_init_soa(uint32_t* d_planes, uint32_t width, uint32_t height, const rt_tiling* tiling,
+                       uint64_t seed_base, rt_stream stream) {
+    (void)height;
+    return render_init(d_planes, width, tiling, seed_base, stream, 1u, "rt_render_init_soa");
 }
 
 // ----- reference-named drop-in launchers (synchronous, void) ----------------------------------------

@@ -66,11 +66,16 @@ class Renderer:
     """One rank's share of a W×H image (all of it when num_ranks = 1)."""
 
     def __init__(self, width: int, height: int, device: int | str = 0, band_rows: int | None = None,
-                 num_ranks: int = 1, rank: int = 0, rng: str = "xorwow"):
+                 num_ranks: int = 1, rank: int = 0, rng: str = "xorwow", state_layout: str = "curand"):
         """rng = "xorwow": the reference's per-pixel cuRAND XORWOW state (parity mode); "philox": stateless
-        per-pixel Philox4x32-10 streams (RT_FLAG_RNG_PHILOX, perf mode, no RNG bytes in HBM)."""
+        per-pixel Philox4x32-10 streams (RT_FLAG_RNG_PHILOX, perf mode, no RNG bytes in HBM).
+        state_layout (XORWOW): "curand" = the reference's 48-byte curandState per pixel; "soa" = the same
+        states as six uint32 planes (RT_FLAG_STATE_SOA, 24 bytes per pixel)."""
         if rng not in ("xorwow", "philox"):
             raise ValueError(f"rng must be 'xorwow' or 'philox', not {rng!r}")
+        if state_layout not in ("curand", "soa"):
+            raise ValueError(f"state_layout must be 'curand' or 'soa', not {state_layout!r}")
+        self.state_layout = state_layout
         self.rng = rng
         self.seed = 1984  # Kernel.cu:175 seed base; the Philox key in perf mode
         self.frame = 0    # Philox frame counter (the XORWOW streams carry over in `state` instead)
@@ -88,8 +93,8 @@ class Renderer:
         # InitCudaBuffers (CudaLayer.cpp:68-74): RGBA8 framebuffer + one 48-byte curandState per pixel
         # (none in Philox mode)
         self.pos = torch.zeros(n, dtype=torch.int32, device=self.device)
-        self.state = (torch.zeros(n * abi.STATE_WORDS, dtype=torch.int32, device=self.device)
-                      if rng == "xorwow" else None)
+        words = n * abi.STATE_WORDS if state_layout == "curand" else 6 * int(lib().rt_soa_plane_words(width, self.local_rows))
+        self.state = torch.zeros(words, dtype=torch.int32, device=self.device) if rng == "xorwow" else None
         self.counters = torch.zeros(16, dtype=torch.int64, device=self.device)
         self.radiance = None
         self.accum = None
@@ -107,8 +112,9 @@ class Renderer:
         if self.state is None:
             return
         t = self.tiling()
-        check(lib().rt_render_init(C.c_void_p(self.state.data_ptr()), self.width, self.height, C.byref(t),
-                                   seed_base, C.c_void_p(self.stream())), "rt_render_init")
+        init = lib().rt_render_init_soa if self.state_layout == "soa" else lib().rt_render_init
+        check(init(C.c_void_p(self.state.data_ptr()), self.width, self.height, C.byref(t), seed_base,
+                   C.c_void_p(self.stream())), "rt_render_init")
 
     def render(self, scene: DeviceScene, spp: int, max_depth: int, inputs: abi.InputStruct, flags: int = 0,
                radiance: bool = False, count: bool = True, frame: int | None = None) -> torch.Tensor:
@@ -133,6 +139,8 @@ class Renderer:
                 if not flags & abi.RT_FLAG_NO_STATE_WRITEBACK:
                     self.frame += 1  # the next frame draws fresh numbers, as the XORWOW streams advance
             a.rng_seed, a.rng_frame = self.seed, frame
+        if self.state_layout == "soa" and self.state is not None:
+            flags |= abi.RT_FLAG_STATE_SOA
         a.flags = flags
         a.tiling = self.tiling()
         a.inputs = inputs
@@ -148,7 +156,16 @@ class Renderer:
         return self.pos.cpu().numpy().view(np.uint32).reshape(self.local_rows, self.width)
 
     def states(self) -> np.ndarray:
-        return self.state.cpu().numpy().view(np.uint32).reshape(-1, abi.STATE_WORDS)
+        """The XORWOW states as (pixels, 12) rt_curand_state words (the SoA planes transposed into words 0-5;
+        words 6-11, the Box-Muller fields the path never uses, zero)."""
+        w = self.state.cpu().numpy().view(np.uint32)
+        if self.state_layout == "curand":
+            return w.reshape(-1, abi.STATE_WORDS)
+        ly, x = np.divmod(np.arange(self.width * self.local_rows), self.width)
+        idx = ((ly >> 3) * ((self.width + 7) >> 3) + (x >> 3)) * 64 + (ly & 7) * 8 + (x & 7)  # soa_index
+        out = np.zeros((idx.size, abi.STATE_WORDS), dtype=np.uint32)
+        out[:, :6] = w.reshape(6, -1)[:, idx].T
+        return out
 
     def radiance_image(self) -> np.ndarray:
         return self.radiance.cpu().numpy().reshape(self.local_rows, self.width, 4)

@@ -214,6 +214,13 @@ typedef struct rt_tiling {
 /* curand_init(seed_base + global_pixel_index, 0, 0) for every local pixel (Kernel.cu:166-176). */
 int rt_render_init(rt_curand_state* d_state, uint32_t width, uint32_t height, const rt_tiling* tiling,
                    uint64_t seed_base, rt_stream stream);
+/* The same states in the native plane layout of RT_FLAG_STATE_SOA: six uint32 planes (d, v[0..4]) of
+ * rt_soa_plane_words(width, local_rows) words each; a plane holds the pixels 8×8 tile by tile (tile
+ * t = (row / 8) · ceil(width / 8) + column / 8 at word t·64 + 8·(row % 8) + column % 8), so the wave that
+ * renders a tile moves 256 contiguous bytes per plane: 24 bytes per pixel, no partial cache lines. */
+uint64_t rt_soa_plane_words(uint32_t width, uint32_t local_rows);
+int rt_render_init_soa(uint32_t* d_planes, uint32_t width, uint32_t height, const rt_tiling* tiling,
+                       uint64_t seed_base, rt_stream stream);
 
 enum rt_render_flags {
     RT_FLAG_FAITHFUL_GRID = 1u << 0, /* skip pixels outside whole 16×16 blocks (Kernel.cu:184) */
@@ -222,19 +229,23 @@ enum rt_render_flags {
     RT_FLAG_RIUS_LEFT_TO_RIGHT = 1u << 3, /* fill Random()'s Vec3(ξ,ξ,ξ) left to right (default: right to
                                              left, the order the survey's g++ build of Math.cuh:233 used) */
     RT_FLAG_COUNT_TESTS = 1u << 4, /* also count box and primitive tests into counters[1], [2] */
-    RT_FLAG_RNG_PHILOX = 1u << 5   /* perf-mode RNG: each pixel draws from the hipRAND/rocRAND Philox4x32-10
+    RT_FLAG_RNG_PHILOX = 1u << 5,  /* perf-mode RNG: each pixel draws from the hipRAND/rocRAND Philox4x32-10
                                       stream rocrand_init(rng_seed, subsequence = global pixel index,
                                       offset = rng_frame << 34) with rocrand_uniform, instead of its cuRAND
                                       XORWOW state.  `state` is neither read nor written (may be NULL): no
                                       per-pixel RNG bytes in HBM.  Not the reference's stream (its images
                                       match the parity mode statistically, not bit for bit). */
+    RT_FLAG_STATE_SOA = 1u << 6    /* `state` holds the XORWOW states as six uint32 planes (rt_render_init_soa)
+                                      instead of rt_curand_state structs: the same streams and images, 24 B
+                                      per pixel read and written with coalesced 4-B accesses (the 48-B
+                                      struct moves whole cache lines for its 24 used bytes) */
 };
 
 typedef struct rt_render_args {
     uint32_t* pos;            /* device RGBA8 framebuffer, local_rows × width (may be NULL if accum given) */
     float* radiance;          /* optional device float[local_rows·width·4]: pre-gamma mean colour (col/spp) */
     float* accum;             /* RT_FLAG_ACCUMULATE: device float4 running sum of samples */
-    rt_curand_state* state;   /* device RNG states, local_rows × width */
+    rt_curand_state* state;   /* device RNG states, local_rows × width (RT_FLAG_STATE_SOA: the six planes) */
     uint64_t* counters;       /* optional device uint64[16]: rays, box tests, primitive tests, primary samples;
                                  with RT_FLAG_COUNT_TESTS also [4..6] = wave-level iterations of node visits,
                                  primitive tests and shading (SIMD-efficiency diagnostics) and, for the v3

@@ -55,3 +55,13 @@ def test_error_reporting_without_device():
     assert lib().rt_scene_create(None, C.byref(h)) == -1
     assert b"NULL" in lib().rt_last_error()
     assert lib().rt_render(None, None, None) == -1
+
+
+def test_soa_plane_words_cover_whole_tiles():
+    """RT_FLAG_STATE_SOA planes hold whole 8x8 tiles (include/rt_hip.h rt_soa_plane_words)."""
+    from cudaraytracer_amd._lib import lib
+    assert lib().rt_soa_plane_words(1920, 1080) == 1920 * 1080
+    assert lib().rt_soa_plane_words(100, 37) == 13 * 5 * 64
+    assert lib().rt_soa_plane_words(7680, 544) == 960 * 68 * 64
+    assert lib().rt_soa_plane_words(1, 1) == 64
+    assert lib().rt_soa_plane_words(0, 5) == 0

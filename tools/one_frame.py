@@ -11,6 +11,7 @@ ap.add_argument("--config", default="c2")
 ap.add_argument("--variant", type=int, default=-1)
 ap.add_argument("--frames", type=int, default=2)
 ap.add_argument("--rng", default="xorwow", choices=("xorwow", "philox"))
+ap.add_argument("--state-layout", default="curand", choices=("curand", "soa"))
 ap.add_argument("--lds-pad", type=int, default=0)
 ap.add_argument("--texel-bytes", type=int, default=3, help="RT_TUNE_TEXEL_LAYOUT (3 = RGB8, 4 = RGBA8)")
 args = ap.parse_args()
@@ -19,7 +20,7 @@ lib().rt_set_variant(args.variant)
 lib().rt_set_tuning(4, args.lds_pad)
 lib().rt_set_tuning(6, args.texel_bytes)
 ds = DeviceScene(cfg.scene_desc())  # c5: three 8192x4096 textures
-r = Renderer(cfg.width, cfg.height, rng=args.rng)
+r = Renderer(cfg.width, cfg.height, rng=args.rng, state_layout=args.state_layout)
 r.render_init()
 flags = abi.RT_FLAG_ACCUMULATE if args.config == "c5" else 0
 for _ in range(args.frames):

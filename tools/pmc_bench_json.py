@@ -1,6 +1,6 @@
 """profiles/pmc_c2_n1.json (read by bench.py) from tools/profile_pmc.sh runs of config 2 with the traffic
 groups (tools/pmc_groups_traffic.txt), one output directory per RNG mode, last (warm) dispatch of each pass.
-    python tools/pmc_bench_json.py <xorwow dir> <philox dir> > profiles/pmc_c2_n1.json
+    python tools/pmc_bench_json.py <xorwow dir> <philox dir> [<xorwow soa-layout dir>] > profiles/pmc_c2_n1.json
 
 Derived fields (MI355X: 8 XCDs, 256 CUs, 1024 SIMDs; SQ_* counters aggregate over SEs, in quad-cycles):
   hbm_read_bytes_corrected = FETCH_SIZE (KB) x 1024 x 2   (gfx950 reports half of the wide reads,
@@ -54,16 +54,21 @@ def summary(out, rng):
 
 
 xorwow, philox = summary(sys.argv[1], "xorwow"), summary(sys.argv[2], "philox")
+soa = summary(sys.argv[3], "xorwow") if len(sys.argv) > 3 else None
 out = {
     "command": "rocprofv3 --pmc <one group per pass: FETCH_SIZE | WRITE_SIZE | SQ_* | TA_*> --kernel-include-regex "
-               "render_kernel -- python3 tools/one_frame.py --variant -1 --frames 3 [--rng philox]  "
+               "render_kernel -- python3 tools/one_frame.py --variant -1 --frames 3 [--rng philox | --state-layout soa]  "
                "(tools/profile_pmc.sh, tools/pmc_groups_traffic.txt; config c2; last, warm dispatch; "
                "tools/pmc_bench_json.py)",
     "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports 1/2 of wide reads). Algorithmic bytes: "
             "XORWOW mode 24 B state in + 24 B out + 4 B RGBA8 per pixel; the kernel touches 24 of each 48-B "
             "curandState (the reference layout), so whole lines move. Philox mode: 4 B per pixel; the 8x8 tile "
-            "per wave writes 32-B row segments, so partial-line writes inflate WRITE_SIZE.",
+            "per wave writes 32-B row segments, so partial-line writes inflate WRITE_SIZE. soa: the same XORWOW "
+            "streams in six uint32 planes (RT_FLAG_STATE_SOA), 24 B read + 24 B written per pixel with coalesced "
+            "4-B accesses.",
     **xorwow,
     "philox": philox,
 }
+if soa:
+    out["soa"] = dict(soa, state_layout="soa")
 print(json.dumps(out, indent=1))
