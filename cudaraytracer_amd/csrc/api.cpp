@@ -252,12 +252,25 @@ struct LaunchEntry {
     std::vector<rt_hittable_desc> hittables;
     std::vector<rt_material_desc> materials;
     std::vector<ImageKey> images;
-    rt_scene* scene = nullptr;
+    // shared with the LaunchKernel calls rendering it: an entry evicted or rebuilt by another thread frees
+    // its device scene only when the last of them has finished
+    std::shared_ptr<rt_scene> scene;
 };
+
+std::shared_ptr<rt_scene> own_scene(rt_scene* s, int device) {
+    return std::shared_ptr<rt_scene>(s, [device](rt_scene* p) {
+        int cur = 0;
+        const bool restore = hipGetDevice(&cur) == hipSuccess;
+        (void)hipSetDevice(device);
+        rt_scene_destroy(p);
+        if (restore) (void)hipSetDevice(cur);
+    });
+}
 
 constexpr size_t kLaunchCacheEntries = 8;
 std::mutex g_launch_mu;
-std::vector<LaunchEntry> g_launch_cache;
+// never destroyed: the entries free device memory, which must not run after the HIP runtime has shut down
+std::vector<LaunchEntry>& g_launch_cache = *new std::vector<LaunchEntry>();
 uint64_t g_launch_clock = 0;
 
 template <class T>
@@ -267,7 +280,7 @@ bool same_bytes(const std::vector<T>& a, const std::vector<T>& b) {
 
 }  // namespace
 
-int reference_scene_for_launch(const void* world, rt_scene** out, double* host_ms) {
+int reference_scene_for_launch(const void* world, std::shared_ptr<rt_scene>* out, double* host_ms) {
     const auto t0 = std::chrono::steady_clock::now();
     int device = 0;
     hipError_t e = hipGetDevice(&device);
@@ -287,12 +300,7 @@ int reference_scene_for_launch(const void* world, rt_scene** out, double* host_m
             if (g_launch_cache.size() >= kLaunchCacheEntries) {  // evict the least recently used entry
                 auto lru = std::min_element(g_launch_cache.begin(), g_launch_cache.end(),
                                             [](const LaunchEntry& a, const LaunchEntry& b) { return a.last_use < b.last_use; });
-                int cur = 0;
-                (void)hipGetDevice(&cur);
-                (void)hipSetDevice(lru->device);
-                rt_scene_destroy(lru->scene);
-                (void)hipSetDevice(cur);
-                g_launch_cache.erase(lru);
+                g_launch_cache.erase(lru);  // (its scene is freed once no call renders it)
             }
             g_launch_cache.emplace_back();
             ent = &g_launch_cache.back();
@@ -311,10 +319,9 @@ int reference_scene_for_launch(const void* world, rt_scene** out, double* host_m
             rt_scene* fresh = nullptr;
             r = create_device_scene(h, &fresh, new_images ? nullptr : ent->scene->texel_block);
             if (r) return r;
-            rt_scene_destroy(ent->scene);
-            ent->scene = fresh;
+            ent->scene = own_scene(fresh, device);
         } else if (!same_bytes(ent->materials, f.materials)) {
-            r = rt_scene_update_materials(ent->scene, f.materials.data(), (uint32_t)f.materials.size());
+            r = rt_scene_update_materials(ent->scene.get(), f.materials.data(), (uint32_t)f.materials.size());
             if (r) return r;
         }
         ent->hittables.swap(f.hittables);

@@ -1931,7 +1931,8 @@ struct PlanKey {
         return tiles < o.tiles;
     }
 };
-std::map<PlanKey, std::shared_ptr<TilePlan>> g_plans;
+// never destroyed: plans free device memory, which must not run after the HIP runtime has shut down
+std::map<PlanKey, std::shared_ptr<TilePlan>>& g_plans = *new std::map<PlanKey, std::shared_ptr<TilePlan>>();
 std::mutex g_plans_mu;
 constexpr size_t kMaxPlans = 32;
 
@@ -2383,7 +2384,7 @@ void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int imag
                   rt_curand_state* d_rand_state, rt_input_struct inputs) {
     // The viewer mutates the graph in place between frames: the cache re-flattens it on
     // every call and updates the device scene by what changed (reference_scene_for_launch, api.cpp).
-    rt_scene* cached = nullptr;
+    std::shared_ptr<rt_scene> cached;  // held until the frame is done (another thread may evict the entry)
     double host_ms = 0.0;
     const int rc = reference_scene_for_launch(world, &cached, &host_ms);
     g_last_host_ms = (float)host_ms;
@@ -2402,7 +2403,7 @@ void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int imag
     a.tiling.rank = 0;
     a.tiling.local_rows = image_height;
     a.inputs = inputs;
-    if (rt_render(cached, &a, nullptr) != RT_OK) return;
+    if (rt_render(cached.get(), &a, nullptr) != RT_OK) return;
     hip_check(hipDeviceSynchronize(), "LaunchKernel: hipDeviceSynchronize");  // Kernel.cu:190
 }
 

@@ -30,7 +30,7 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
 // (device, world): materials edited in place are re-uploaded, geometry edits rebuild the BVH and tables but
 // keep the uploaded texels, a new image (data pointer, width or height, CudaLayer.cpp:889-903) re-uploads
 // them.  *host_ms: host time spent (flatten + compare + any update).
-int reference_scene_for_launch(const void* world, rt_scene** out, double* host_ms);
+int reference_scene_for_launch(const void* world, std::shared_ptr<rt_scene>* out, double* host_ms);
 
 }  // namespace rt
 

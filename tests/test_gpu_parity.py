@@ -563,3 +563,53 @@ def test_soa_state_layout_is_the_same_stream(name, variant):
     a2.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(full, a2.image())
+
+
+def test_launch_kernel_cache_eviction_across_threads():
+    """Two host threads drive LaunchKernel over 10 reference graphs (the scene cache holds 8 per device, so
+    entries are evicted while the other thread renders them): every frame equals the single-thread frame."""
+    import threading
+
+    case = CASE_BY_NAME["default_world_160x120_s8"]
+    cfg = case.cfg().scaled(64, 48, 2)
+    W, H = cfg.width, cfg.height
+    dev = torch.device("cuda", 0)
+    graphs = []
+    for k in range(10):
+        sc = scenes.builtin(cfg.scene)
+        g = refgraph.build_graph(sc)
+        m = g.keep[[i for i, o in enumerate(g.keep) if isinstance(o, refgraph.Constant)][1]]
+        m.color.e[0] = k / 10.0  # ten distinct scenes
+        graphs.append(g)
+
+    def frame(g):
+        pos = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        state = torch.zeros(W * H * abi.STATE_WORDS, dtype=torch.int32, device=dev)
+        lib().LaunchRenderInit(abi.Dim3(W // 16, H // 16, 1), abi.Dim3(16, 16, 1), W, H, C.c_void_p(state.data_ptr()))
+        lib().LaunchKernel(C.c_void_p(pos.data_ptr()), W, H, cfg.spp, cfg.depth, C.c_void_p(C.addressof(g.world)),
+                           C.c_void_p(state.data_ptr()), cfg.inputs())
+        torch.cuda.synchronize()
+        return pos.cpu().numpy().copy()
+
+    want = [frame(g) for g in graphs]
+    got = {}
+    errors = []
+
+    def worker(t):
+        try:
+            torch.cuda.set_device(0)
+            for rep in range(3):
+                for k in range(t, 10, 2):
+                    got[(t, rep, k)] = frame(graphs[k])
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors
+    assert len(got) == 30
+    for (t, rep, k), img in got.items():
+        np.testing.assert_array_equal(img, want[k])
