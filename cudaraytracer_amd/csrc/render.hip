@@ -241,7 +241,12 @@ constexpr int kBlock = 256;
 // v4 work queue: the frame's work indices are split into this many contiguous ranges, each with its own
 // head 128 B from the next — one shared head serialises every wave's atomic in one L2 channel (≈ 16 ns
 // each: 0.5 ms for the 32400 chunks of a 1080p frame, the whole C5 frame time)
-constexpr uint32_t kQueueCounters = 64;
+#ifndef RT_QUEUE_HEADS
+#define RT_QUEUE_HEADS 16
+#endif
+constexpr uint32_t kQueueCounters = RT_QUEUE_HEADS;  // <= 32: one word marks the exhausted heads
+static_assert(kQueueCounters >= 1 && kQueueCounters <= 32, "queue heads");
+constexpr uint32_t kQueueAllDone = kQueueCounters == 32 ? 0xffffffffu : (1u << kQueueCounters) - 1u;
 
 // Traversal stack of each kernel family: per-lane scratch array (v1, any scene), 32-bit LDS entries
 // (v2, 32-bit references), 16-bit LDS entries (v3/v4, scenes whose references fit 16 bits)
@@ -1703,11 +1708,18 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                     base = __builtin_amdgcn_readlane(base, leader);
                     const uint32_t idx = qc * P.work_per_counter + base;
                     if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
-                        if (++qtried >= kQueueCounters) {
+                        // mark it in the exhausted-heads word and move to the next live head (so a wave
+                        // probes a few heads at the frame's end, not every one of them)
+                        uint32_t done = 0u;
+                        if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * 32u, 1u << qc);
+                        done = __builtin_amdgcn_readlane(done, leader) | (1u << qc);
+                        if (done == kQueueAllDone || ++qtried >= kQueueCounters) {
                             drained = true;
                             break;
                         }
-                        qc = qc + 1u == kQueueCounters ? 0u : qc + 1u;
+                        const uint32_t live = ~done & kQueueAllDone;        // (nonzero here)
+                        const uint32_t above = live & ~((2u << qc) - 1u);   // live heads after qc
+                        qc = (uint32_t)__builtin_ctz(above ? above : live);
                         continue;
                     }
                     wq_next = idx;
@@ -1976,7 +1988,7 @@ constexpr size_t kLdsLimit = 160 * 1024;
 // on the launch's stream right before it.  Slots are 64 B apart; a slot is reused only after
 // kQueueSlots further launches on that device, far more than can be in flight at once.
 constexpr uint32_t kQueueSlots = 256;
-constexpr uint32_t kQueueBytes = dev::kQueueCounters * 128u;  // one launch's queue heads
+constexpr uint32_t kQueueBytes = (dev::kQueueCounters + 1u) * 128u;  // one launch's heads + exhausted-heads word
 constexpr int kMaxDevices = 64;
 struct QueueRing {
     uint32_t* buf = nullptr;
