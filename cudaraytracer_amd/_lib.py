@@ -42,6 +42,7 @@ EXPORTED = [
     "rt_set_wave_trace",
     "rt_set_tile_order",
     "rt_last_kernel_ms",
+    "rt_last_variant",
     "rt_last_launch_host_ms",
     "rt_set_variant",
     "rt_set_tuning",
@@ -89,6 +90,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_set_wave_trace.argtypes = [C.c_void_p]
     lib.rt_set_tile_order.argtypes = [C.c_void_p]
     lib.rt_last_kernel_ms.restype = C.c_float
+    lib.rt_last_variant.restype = C.c_int
     lib.rt_last_launch_host_ms.restype = C.c_float
     lib.rt_set_variant.argtypes = [C.c_int]
     lib.rt_set_tuning.argtypes = [C.c_int, C.c_int]

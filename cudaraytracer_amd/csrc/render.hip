@@ -29,6 +29,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <tuple>
 #include <type_traits>
 
 #include "rt_internal.h"
@@ -1856,6 +1857,7 @@ thread_local bool g_timing = false;
 thread_local float g_last_ms = -1.0f;
 thread_local float g_last_host_ms = -1.0f;  // LaunchKernel: host time of the scene-cache step
 thread_local int g_variant = -1;
+thread_local int g_last_variant = -1;  // the variant the last rt_render on this thread launched
 
 int hip_check(hipError_t e, const char* what, int code = RT_ERR_DEVICE) {
     if (e == hipSuccess) return RT_OK;
@@ -1956,6 +1958,37 @@ struct PlanKey {
         return tiles < o.tiles;
     }
 };
+// Automatic kernel choice below 64 spp, by measurement.  Which of v3 (tile waves, longest-first order) and v4
+// (persistent, per-lane pixel queue) is faster there depends on the scene as much as on spp (config 2's scene
+// at 4 spp: v3 1.54 vs v4 1.77 ms; config 5's at 4 spp: 0.89 vs 0.65; config 3's at 8 spp: 14.1 vs 12.8,
+// profiles/r02_ab_v3_v4_low_spp.txt).  Both render the same bits, so the library times one frame of each
+// for a (device, stream, scene, frame shape, spp, depth, RNG mode) and keeps the faster: the first frame
+// runs v3 untimed (it builds the tile order), the second v3 timed, the third v4 timed, and the choice is
+// made once both timings have completed (until then: v4 below 32 spp, v3 from 32).
+struct AutoKey {
+    int device;
+    void* stream;
+    const void* scene;
+    uint32_t width, rows, spp, depth, philox;
+    bool operator<(const AutoKey& o) const {
+        return std::tie(device, stream, scene, width, rows, spp, depth, philox) <
+               std::tie(o.device, o.stream, o.scene, o.width, o.rows, o.spp, o.depth, o.philox);
+    }
+};
+struct AutoChoice {
+    int stage = 0;      // frames of the trial already launched
+    int chosen = -1;    // the decided variant
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // v3 start/end, v4 start/end
+    ~AutoChoice() {
+        for (hipEvent_t& e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+constexpr uint32_t kAutoSpp = 64;  // from here on v3 always (configs 2-4: 64-256 spp)
+std::mutex g_auto_mu;
+// never destroyed (holds HIP events, see g_plans)
+std::map<AutoKey, std::unique_ptr<AutoChoice>>& g_auto = *new std::map<AutoKey, std::unique_ptr<AutoChoice>>();
+
 // never destroyed: plans free device memory, which must not run after the HIP runtime has shut down
 std::map<PlanKey, std::shared_ptr<TilePlan>>& g_plans = *new std::map<PlanKey, std::shared_ptr<TilePlan>>();
 std::mutex g_plans_mu;
@@ -2056,6 +2089,8 @@ int rt_set_variant(int variant) {
     g_variant = variant;
     return prev;
 }
+
+int rt_last_variant(void) { return g_last_variant; }
 
 int rt_set_tuning(int key, int value) {
     if (key == RT_TUNE_REGEN_THRESHOLD) {
@@ -2240,8 +2275,47 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // 2's wave in 5 KB of LDS, 8 waves per SIMD (config 2: 17.05 vs 17.8 ms with 15-word parking; config 3,
     // depth 16: 365 vs 408 ms for v4).  Compact parking falls back to 15 words where its packed counters
     // would overflow.
-    if (variant < 0 || variant >= kNumVariants)
+    AutoChoice* trial = nullptr;  // this frame is timed for the automatic choice: events ev[trial_slot..+1]
+    int trial_slot = 0;
+    const bool automatic = variant < 0 || variant >= kNumVariants;
+    if (automatic) {
         variant = a->samples_per_pixel < 32 ? kVarV4 : kVarV3Compact;
+        if (a->samples_per_pixel > 0 && a->samples_per_pixel < kAutoSpp && a->max_depth > 0) {
+            int device = 0;
+            (void)hipGetDevice(&device);
+            const AutoKey key{device, stream, scene, a->width, T.local_rows, a->samples_per_pixel, a->max_depth,
+                              philox ? 1u : 0u};
+            std::lock_guard<std::mutex> lock(g_auto_mu);
+            auto it = g_auto.find(key);
+            if (it == g_auto.end()) {
+                if (g_auto.size() >= 64) g_auto.clear();
+                it = g_auto.emplace(key, std::make_unique<AutoChoice>()).first;
+            }
+            AutoChoice& ac = *it->second;
+            if (ac.chosen >= 0) {
+                variant = ac.chosen;
+            } else if (ac.stage < 3) {
+                variant = ac.stage < 2 ? kVarV3Compact : kVarV4;
+                if (ac.stage >= 1) {
+                    trial_slot = ac.stage == 1 ? 0 : 2;
+                    if ((ac.ev[trial_slot] || hipEventCreate(&ac.ev[trial_slot]) == hipSuccess) &&
+                        (ac.ev[trial_slot + 1] || hipEventCreate(&ac.ev[trial_slot + 1]) == hipSuccess))
+                        trial = &ac;
+                }
+                ac.stage++;
+            } else if (ac.ev[1] && ac.ev[3] && hipEventQuery(ac.ev[1]) == hipSuccess &&
+                       hipEventQuery(ac.ev[3]) == hipSuccess) {
+                float t3 = -1.0f, t4 = -1.0f;
+                (void)hipEventElapsedTime(&t3, ac.ev[0], ac.ev[1]);
+                (void)hipEventElapsedTime(&t4, ac.ev[2], ac.ev[3]);
+                ac.chosen = (t3 >= 0.0f && t4 >= 0.0f && t4 < t3) ? kVarV4 : kVarV3Compact;
+                variant = ac.chosen;
+            } else if (!ac.ev[1] || !ac.ev[3]) {
+                ac.chosen = variant;  // no events: keep the static rule
+            }
+            (void)hipGetLastError();  // (hipEventQuery reports hipErrorNotReady while pending)
+        }
+    }
     const bool refs16_fit = S.num_nodes < (uint32_t)dev::kSentinel16 && S.num_prims < 8192u;
     if (kVariants[variant].stack == dev::STACK_LDS16 && !refs16_fit) {
         if (philox) {
@@ -2321,6 +2395,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0, s);
     }
+    g_last_variant = variant;
+    if (trial) (void)hipEventRecord(trial->ev[trial_slot], s);
     (void)hipGetLastError();
     hipLaunchKernelGGL(fn, dim3(grid), dim3(V.block), lds_bytes, s, P);
     int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
@@ -2330,6 +2406,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         rc = hip_check(hipGetLastError(), "rt_render: plan kernel launch", RT_ERR_LAUNCH);
         if (rc == RT_OK) plan->valid.store(true);
     }
+    if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);
     if (g_timing) {
         (void)hipEventRecord(e1, s);
         if (rc == RT_OK && hipEventSynchronize(e1) == hipSuccess) {

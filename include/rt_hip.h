@@ -285,12 +285,15 @@ int rt_set_wave_trace(void* buffer);
  * order (NULL = row-major).  Results do not depend on it (every pixel is independent); the time does. */
 int rt_set_tile_order(const void* order);
 
-/* Tuning/benchmark knob (per thread): the kernel rt_render launches.  -1 = automatic (3 for spp >= 32, else 4,
- * with fallbacks where a kernel's limits are exceeded); 0 = v1 (scratch stack, any scene), 1 = v2 (resumable,
- * 32-bit LDS stacks), 2 = v3 (resumable, path state parked in LDS, 16-bit stacks, longest-first tile order),
- * 3 = v3 with compact parking, 4 = v4 (v3 made persistent with a pixel work queue).  Returns the previous
- * value. */
+/* Tuning/benchmark knob (per thread): the kernel rt_render launches.  -1 = automatic: 3 from 64 spp; below,
+ * the faster of 3 and 4 as timed on the first frames of each (device, stream, scene, frame shape, spp, depth,
+ * RNG mode) — both render identical bits — with fallbacks where a kernel's limits are exceeded; 0 = v1
+ * (scratch stack, any scene), 1 = v2 (resumable, 32-bit LDS stacks), 2 = v3 (resumable, path state parked in
+ * LDS, 16-bit stacks, longest-first tile order), 3 = v3 with compact parking, 4 = v4 (v3 made persistent with
+ * a pixel work queue).  Returns the previous value. */
 int rt_set_variant(int variant);
+/* The variant the last rt_render on this thread launched (-1 before any). */
+int rt_last_variant(void);
 
 /* Tuning knob (per thread); returns the previous value or a negative rt_status.
  *   RT_TUNE_REGEN_THRESHOLD: resumable kernels leave traversal to shade/regenerate finished lanes when

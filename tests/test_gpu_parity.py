@@ -613,3 +613,32 @@ def test_launch_kernel_cache_eviction_across_threads():
     assert len(got) == 30
     for (t, rep, k), img in got.items():
         np.testing.assert_array_equal(img, want[k])
+
+
+@pytest.mark.parametrize("config, spp", [("c2", 2), ("c2", 8), ("c3", 4)])
+def test_automatic_choice_times_both_kernels_and_keeps_the_bits(config, spp):
+    """Below 64 spp the automatic choice runs v3 (untimed, then timed) and v4 (timed) on the first frames of
+    a frame shape and keeps the faster; every frame of the sequence is the same image (NO_STATE_WRITEBACK)."""
+    cfg = scenes.CONFIGS[config].scaled(480, 272, spp)
+    lib().rt_set_variant(-1)
+    ds = DeviceScene(scenes.builtin(cfg.scene))
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    images, used = [], []
+    for _ in range(8):
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
+        used.append(lib().rt_last_variant())
+        torch.cuda.synchronize()
+        images.append(r.image().copy())
+    assert used[:3] == [3, 3, 4], used
+    assert used[4:] == [used[4]] * 4 and used[4] in (3, 4), used  # decided by frame 5 (all trials completed)
+    for img in images[1:]:
+        np.testing.assert_array_equal(img, images[0])
+    lib().rt_set_variant(4)
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
+    assert lib().rt_last_variant() == 4
+    r.render(ds, 64, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)  # explicit choice holds
+    assert lib().rt_last_variant() == 4
+    lib().rt_set_variant(-1)
+    r.render(ds, 64, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
+    assert lib().rt_last_variant() == 3  # from 64 spp: v3
