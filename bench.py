@@ -19,6 +19,7 @@ kernel itself (one closest-hit query = one iteration of color()'s loop, Kernel.c
 from __future__ import annotations
 
 import argparse
+import re
 import json
 import math
 import os
@@ -277,7 +278,8 @@ def main() -> None:
             "data": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
             "config": {
                 "workload": (f"{args.config}: {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}, "
-                             f"{scenes.CONFIGS[args.config].description.split(', ', 3)[-1]}"),
+                             + ", ".join(part for part in scenes.CONFIGS[args.config].description.split(", ")
+                                         if not re.match(r"\d+ GPUs$|\d+x\d+$|\d+ spp|depth \d+$", part))),
                 "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
                 "parallelism": (f"{world} rank(s) x 16-row bands + {'RCCL' if args.backend == 'nccl' else args.backend} gather"
                                 if world > 1 else "1 GPU"),

@@ -21,6 +21,8 @@ ap.add_argument("--variants", default="-1", help="kernel variants to time (rt_se
 ap.add_argument("--configs", default="c3,c4,c5")
 ap.add_argument("--rngs", default="xorwow,philox")
 ap.add_argument("--texel-layouts", default="3,4", help="c5: device bytes per texel (RT_TUNE_TEXEL_LAYOUT)")
+ap.add_argument("--state-layouts", default="curand",
+                help="XORWOW state layouts to time: curand (the reference's 48-B structs), soa (native planes)")
 args = ap.parse_args()
 
 
@@ -45,17 +47,19 @@ def scene_for(config, layout):
     return _scenes[key]
 
 
-def run(variant, config, rng, layout=3):
+def run(variant, config, rng, layout=3, state_layout="curand"):
     lib().rt_set_variant(variant)
     cfg = scenes.CONFIGS[config]
     ds = scene_for(config, layout)
     out = {"config": config, "rng": rng, "variant": variant,
            "workload": f"{cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}"}
+    if rng == "xorwow":
+        out["state_layout"] = state_layout
     if config == "c5":
         out["texel_bytes"] = layout
         out["texture_size"] = list(cfg.texture_size)
     if config == "c5":
-        r = Renderer(cfg.width, cfg.height, rng=rng)
+        r = Renderer(cfg.width, cfg.height, rng=rng, state_layout=state_layout)
         r.render_init()
         frames, times = 60, []
         r.counters.zero_()
@@ -72,7 +76,7 @@ def run(variant, config, rng, layout=3):
     if config == "c4":
         kw = dict(band_rows=16, num_ranks=8, rank=0)
         out["workload"] += ", rank 0 of 8 (16-row bands)"
-    r = Renderer(cfg.width, cfg.height, rng=rng, **kw)
+    r = Renderer(cfg.width, cfg.height, rng=rng, state_layout=state_layout, **kw)
     r.render_init()
     r.render(ds, 1, cfg.depth, cfg.inputs())  # warm-up
     torch.cuda.synchronize()
@@ -87,4 +91,5 @@ for v in (int(x) for x in args.variants.split(",")):
     for config in args.configs.split(","):
         for rng in args.rngs.split(","):
             for layout in ([int(x) for x in args.texel_layouts.split(",")] if config == "c5" else [3]):
-                print(json.dumps(run(v, config, rng, layout)), flush=True)
+                for sl in (args.state_layouts.split(",") if rng == "xorwow" else ["curand"]):
+                    print(json.dumps(run(v, config, rng, layout, sl)), flush=True)

@@ -2,7 +2,7 @@
 # One GPU session (run through gpurun from the repo root): parity tests, smoke, bench + rocprofv3 kernel
 # summary, per-config timings.  Every GPU step has its own time limit and the session stops at the first
 # GPU fault, abort, segfault or timeout (pytest rc 1 = test failures only, which does not stop it).
-#   STEPS="tests smoke bench prof configs"   (default: all)   PYTEST_ARGS=...   BENCH_ARGS=...
+#   STEPS="tests smoke bench prof configs rehearse"   (default: all but rehearse)   PYTEST_ARGS=...   BENCH_ARGS=...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -23,6 +23,15 @@ for step in $STEPS; do
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
         python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench_prof.log 2>&1 || exit $? ;;
+    rehearse)  # bench.py's N > 1 path with every rank on device 0 (gloo gather): weak (C2) and strong (C4) scaling
+      for n in ${REHEARSE_N:-2 4}; do
+        for cfg in c2 c4; do
+          timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+            --master-port $((29400 + n)) bench.py --gpus $n --steps 3 --warmup 1 --config $cfg --backend gloo \
+            --share-gpu --no-cpu-baseline --no-philox-line > gpurun_out/rehearse_${cfg}_n$n.log 2>&1 || exit $?
+          tail -1 gpurun_out/rehearse_${cfg}_n$n.log
+        done
+      done ;;
     configs)
       timeout -k 10 400 python tools/bench_configs.py ${CONFIGS_ARGS:-} > gpurun_out/configs.log 2>&1 || exit $?
       cat gpurun_out/configs.log | grep -v amdgpu.ids ;;
