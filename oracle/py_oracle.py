@@ -58,6 +58,7 @@ def _declare(L: C.CDLL) -> C.CDLL:
     if True:
         vp = C.c_void_p
         L.orc_curand_init.argtypes = [C.c_ulonglong, vp]
+        L.orc_xorwow_seed.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_uint, C.c_uint, vp]
         L.orc_curand.argtypes = [vp]
         L.orc_curand.restype = C.c_uint
         L.orc_curand_uniform.argtypes = [vp]

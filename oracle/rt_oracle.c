@@ -68,11 +68,17 @@ static inline int refract(v3 v, v3 n, float ni_over_nt, v3* refracted) {
 /* CMakeLists.txt:28): _curand_init_scratch seeding, curand() xorwow step, _curand_uniform.        */
 /* Called with subsequence 0 and offset 0 (Kernel.cu:163,175), so no skip-ahead matrices apply.   */
 /* ---------------------------------------------------------------------------------------------- */
-void orc_curand_init(unsigned long long seed, rt_curand_state* s) {
-    unsigned int s0 = ((unsigned int)seed) ^ 0xaad26b49u;
-    unsigned int s1 = ((unsigned int)(seed >> 32)) ^ 0xf7dcefddu;
-    unsigned int t0 = 1099087573u * s0;
-    unsigned int t1 = 2591861531u * s1;
+/* The xorwow seeding scheme shared by cuRAND and rocRAND: the 64-bit seed's halves are scrambled by two
+   xor constants and two multipliers into (d, v[5]) around Marsaglia's base state.  The two libraries differ
+   only in those four constants (rocRAND: rocrand_xorwow.h:113-116), so checking this function with
+   rocRAND's constants against rocRAND's own engine (tests/golden/rocrand_xorwow_kat.json) pins the base
+   state, the Weyl step and the recurrence of orc_curand independently of the survey probe. */
+void orc_xorwow_seed(unsigned long long seed, unsigned int xor0, unsigned int xor1, unsigned int mul0,
+                     unsigned int mul1, rt_curand_state* s) {
+    unsigned int s0 = ((unsigned int)seed) ^ xor0;
+    unsigned int s1 = ((unsigned int)(seed >> 32)) ^ xor1;
+    unsigned int t0 = mul0 * s0;
+    unsigned int t1 = mul1 * s1;
     s->d = 6615241u + t1 + t0;
     s->v[0] = 123456789u + t0;
     s->v[1] = 362436069u ^ t0;
@@ -84,6 +90,10 @@ void orc_curand_init(unsigned long long seed, rt_curand_state* s) {
     s->boxmuller_extra = 0.0f;
     s->pad_ = 0;
     s->boxmuller_extra_double = 0.0;
+}
+
+void orc_curand_init(unsigned long long seed, rt_curand_state* s) {
+    orc_xorwow_seed(seed, 0xaad26b49u, 0xf7dcefddu, 1099087573u, 2591861531u, s);
 }
 
 unsigned int orc_curand(rt_curand_state* s) {

@@ -22,6 +22,8 @@ extern "C" {
 typedef struct orc_scene orc_scene;
 
 /* cuRAND XORWOW restatement (curand_kernel.h, CUDA toolkit >= 12.0; not vendored in the reference). */
+void orc_xorwow_seed(unsigned long long seed, unsigned int xor0, unsigned int xor1, unsigned int mul0,
+                     unsigned int mul1, rt_curand_state* state);
 void orc_curand_init(unsigned long long seed, rt_curand_state* state);
 unsigned int orc_curand(rt_curand_state* state);
 float orc_curand_uniform(rt_curand_state* state);

@@ -57,6 +57,22 @@ def test_c1_left_to_right_order_differs_from_probe():
     assert pos[112, 200] != 0xFF7F5F3C and cnt.rays != 868442
 
 
+def test_xorwow_recurrence_matches_rocrand_engine():
+    """tests/golden/rocrand_xorwow_kat.json is rocRAND's own xorwow engine (make_rocrand_xorwow_kat.cpp): the
+    oracle's seeding with rocRAND's four constants must give rocRAND's state, and orc_curand (cuRAND's
+    curand(), the recurrence both libraries share) its outputs.  cuRAND's own four seeding constants are
+    pinned by the survey probe above."""
+    with open(os.path.join(GOLDEN, "rocrand_xorwow_kat.json")) as f:
+        kat = json.load(f)
+    k = kat["seeding_constants"]
+    assert len(kat["streams"]) >= 8
+    for v in kat["streams"]:
+        st = abi.CurandState()
+        po.lib().orc_xorwow_seed(v["seed"], k["xor0"], k["xor1"], k["mul0"], k["mul1"], C.byref(st))
+        assert [st.d] + list(st.v) == v["init"], v["seed"]
+        assert [po.lib().orc_curand(C.byref(st)) for _ in range(len(v["raw"]))] == v["raw"], v["seed"]
+
+
 # ---------------------------------------------------------------------------------------------------
 # Golden fixtures (regression of the restatement; tests/golden/make_golden.py)
 # ---------------------------------------------------------------------------------------------------
