@@ -1261,6 +1261,9 @@ __device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col,
 typedef const __attribute__((address_space(4))) float ConstF32;
 typedef const __attribute__((address_space(4))) uint32_t ConstU32;
 typedef const __attribute__((address_space(4))) uint8_t ConstU8;
+#ifndef RT_DIAG_NONE
+#define RT_DIAG_NONE 0
+#endif
 #ifndef RT_SLAB_ASM
 #define RT_SLAB_ASM 1
 #endif
@@ -1324,6 +1327,9 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             asm("" : "+v"(top1));
             asm("" : "+v"(top2));
             float c0min, c0max, c1min, c1max;
+#if RT_DIAG_NONE
+            float c0maxi = 0.0f, c1maxi = 0.0f;  // far distances without the t_best clip (diagnostic)
+#endif
             uint32_t ch0, ch1;
             // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0) for a
             // positive direction component and (0, 1/d) for a negative one,
@@ -1350,6 +1356,10 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 c0max = vmin3(fx0, fy0, vmin(fz0, t_best_c)) * kSlabSlack;
                 c1min = vmax3(nx1, ny1, vmax(tmin_s, nz1));
                 c1max = vmin3(fx1, fy1, vmin(fz1, t_best_c)) * kSlabSlack;
+#if RT_DIAG_NONE
+                c0maxi = vmin3(fx0, fy0, fz0) * kSlabSlack;
+                c1maxi = vmin3(fx1, fy1, fz1) * kSlabSlack;
+#endif
 #else
                 c0min = fmaxf(fmaxf(nx0, ny0), fmaxf(nz0, kTmin));
                 c0max = fminf(fminf(fx0, fy0), fminf(fz0, t_best_c)) * kSlabSlack;
@@ -1392,11 +1402,22 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 cnt.wnode += wave_leader();
                 if (__ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0) cnt.wnode_uniform += wave_leader();
                 const uint32_t act = (uint32_t)__popcll(__ballot(1));
+#if RT_DIAG_NONE
+                // diagnostic build: counters 13/14 = visits whose two children both miss / ... that would be
+                // hit without the t_best clip (the visits a popped-entry distance test could skip)
+                {
+                    const bool nn = !(c0min <= c0max) && !(c1min <= c1max);
+                    cnt.idle_nt += nn ? 1u : 0u;
+                    cnt.idle_fin += (nn && (c0min <= c0maxi || c1min <= c1maxi)) ? 1u : 0u;
+                }
+                if (wave_leader()) cnt.idle_wait += n_outer - act;
+#else
                 if (wave_leader()) {
                     cnt.idle_nt += 64u - ntrav;
                     cnt.idle_fin += ntrav - n_outer;
                     cnt.idle_wait += n_outer - act;
                 }
+#endif
             }
             const bool h0 = c0min <= c0max;
             const bool h1 = c1min <= c1max;
