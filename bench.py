@@ -37,6 +37,7 @@ from cudaraytracer_amd._lib import lib  # noqa: E402
 from cudaraytracer_amd.renderer import DeviceScene, Renderer  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ≈ 8 TB/s per GPU
 # SURVEY.md §8(d) D4 counted-flop model: AABB test 21, sphere test 23, shading/sky/sampling 60 per ray,
 # camera ray 40 per primary sample.
 FLOP_BOX, FLOP_PRIM, FLOP_RAY, FLOP_PRIMARY = 21, 23, 60, 40
@@ -257,8 +258,19 @@ def main() -> None:
 
     if rank == 0:
         achieved = f_launch / (kernel_ms * 1e-3) / 1e12
-        pmc = pmc_profile(args.config, args.rng, args.state_layout) if args.config == "c2" and world == 1 else {}
+        # HBM bytes per launch: the committed N=1 C2 PMC summary.  A rank's bytes do not depend on spp (per pixel:
+        # RNG state in and out, one RGBA8 store), so other frame shapes scale it by the rank's pixel count.
+        pmc = pmc_profile("c2", args.rng, args.state_layout)
+        c2 = scenes.CONFIGS["c2"]
+        pix_scale = r.local_rows * cfg.width / (c2.width * c2.height)
+        if "hbm_bytes_per_launch" in pmc and pix_scale != 1.0:
+            for k in ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch"):
+                if k in pmc:
+                    pmc[k] = round(pmc[k] * pix_scale)
+            pmc["scaled"] = True
         rays_per_launch = c[0]
+        hbm_gbps = (round(pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 2)
+                    if "hbm_bytes_per_launch" in pmc else None)
         metric = ("Mray/s (and ms/frame) at 1920x1080, 64 spp, depth 8, random-spheres" if not strong else
                   "Mray/s (and ms/frame) at 7680x4320, 128 spp, depth 8, random-spheres (8-GPU tile-split config)")
         line = {
@@ -295,10 +307,13 @@ def main() -> None:
                 "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                 "traffic": pmc.get("hbm_bytes_per_launch"),
-                "traffic_source": "rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_c2_n1.json" if pmc else None,
+                "traffic_source": (("rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_c2_n1.json"
+                                    + (" (per-pixel bytes x this rank's pixels)" if pmc.get("scaled") else ""))
+                                   if "hbm_bytes_per_launch" in pmc else None),
                 "algorithmic_hbm_bytes": pmc.get("algorithmic_bytes_per_launch"),
-                "hbm_GBps_achieved": (round(pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 2)
-                                      if "hbm_bytes_per_launch" in pmc else None),
+                "hbm_GBps_achieved": hbm_gbps,
+                "hbm_frac_of_peak": round(hbm_gbps / PEAK_HBM_GBPS, 5) if hbm_gbps is not None else None,
+                "hbm_per_rank": world > 1,
                 "simd_lane_utilization": pmc.get("valu_lane_utilization"),
                 "waves_per_simd": pmc.get("avg_waves_per_simd"),
                 "ta_busy_frac": pmc.get("ta_busy_frac_per_cu"),
