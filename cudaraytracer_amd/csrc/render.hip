@@ -198,10 +198,6 @@ __device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
 // Kernel parameters (by value; everything launch-uniform precomputed on the host with the same
 // binary32 operations the reference performs per thread).
 // ---------------------------------------------------------------------------------------------------
-// Pixel order regions (RT_TUNE_PIXEL_SORT): 2^region_log2 pixels square, 32 × 32 (16 waves) for a whole frame,
-// 16 × 16 for a rank of a multi-rank band split with 16-row bands (a region stays inside one band)
-using PermT = uint16_t;
-
 struct KParams {
     const float4* nodes;
     const float4* nodes48;   // v3: three box float4 per node
@@ -239,11 +235,6 @@ struct KParams {
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
-    const PermT* pixel_perm;         // v3: per R × R region (R = 2^region_log2), lane l of the region's k-th wave
-                                     //     renders region pixel pixel_perm[R²·region + 64·k + l] (row·R + column);
-                                     //     NULL = 8×8 tiles
-    uint16_t* pixel_rays;            // v3: per local pixel, the rays it traced in this launch (for the next sort)
-    uint32_t region_log2;            // v3: 4 or 5 (with pixel_perm)
 };
 
 constexpr int kStackMax = 64;
@@ -732,22 +723,8 @@ __device__ __forceinline__ bool lane_pixel(const KParams& P, uint32_t& x, uint32
     const uint32_t bx = tile % P.tiles_x, by = tile / P.tiles_x;
     uint32_t ly;
     if constexpr (BLOCK == 64) {
-        if (P.pixel_perm) {
-            // tile (bx, by) is the k-th existing 8×8 tile of its region (a region on the right edge of the tile
-            // grid may have fewer columns of tiles): its wave renders the region's pixels ranked k·64 … k·64 + 63
-            // by the previous launch's ray counts (pixel_sort_kernel)
-            const uint32_t rl = P.region_log2, ts = rl - 3u, rtiles = 1u << ts;
-            const uint32_t rx = bx >> ts, ry = by >> ts;
-            const uint32_t kx = bx & (rtiles - 1u), ky = by & (rtiles - 1u);
-            const uint32_t nx = min(rtiles, P.tiles_x - (rx << ts));
-            const uint32_t region = ry * ((P.tiles_x + rtiles - 1u) >> ts) + rx;
-            const uint32_t q = P.pixel_perm[(region << (2u * rl)) + (ky * nx + kx) * 64u + lane];
-            x = (rx << rl) + (q & ((1u << rl) - 1u));
-            ly = (ry << rl) + (q >> rl);
-        } else {
-            x = bx * 8 + (lane & 7u);
-            ly = by * 8 + (lane >> 3);
-        }
+        x = bx * 8 + (lane & 7u);
+        ly = by * 8 + (lane >> 3);
     } else {
         x = bx * 16 + (wave & 1u) * 8 + (lane & 7u);
         ly = by * 16 + (wave >> 1) * 8 + (lane >> 3);
@@ -1647,7 +1624,6 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
     cnt.rays = rays;
     cnt.primary = P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
-    if (P.pixel_rays) P.pixel_rays[pix] = (uint16_t)(rays > 0xffffu ? 0xffffu : rays);
     finish_pixel<COUNT_TESTS>(P, pix, state_at(P, pix), rng, col, cnt);
 }
 
@@ -1887,44 +1863,6 @@ __global__ __launch_bounds__(1024) void plan_order_kernel(const uint32_t* __rest
     for (uint32_t i = threadIdx.x; i < n; i += 1024u) order[atomicAdd(&start[cost_bucket(cost[i])], 1u)] = i;
 }
 
-// Pixel order of the next v3 launch, one workgroup per region: the region's pixels sorted by the rays each
-// traced in this launch, costliest first (ties: 8×8-tile order), so that each of the region's waves renders
-// pixels of similar cost — a wave lives as long as its slowest pixel.  Pixels outside the (local) image sort
-// last; a region holds at most 64 image pixels per existing tile, so they all land in existing tiles' ranks.
-template <uint32_t kRegion>
-__global__ __launch_bounds__(kRegion * kRegion) void pixel_sort_kernel(const uint16_t* __restrict__ rays,
-                                                                       PermT* __restrict__ perm, uint32_t width,
-                                                                       uint32_t rows, uint32_t regions_x) {
-    constexpr uint32_t kRegionTiles = kRegion / 8, kRegionPixels = kRegion * kRegion;
-    constexpr uint32_t kBits = kRegionPixels <= 256 ? 8u : 10u;
-    __shared__ uint32_t key[kRegionPixels];
-    const uint32_t i = threadIdx.x, region = blockIdx.x;  // i: the pixel's rank in 8×8-tile order
-    const uint32_t t = i >> 6;
-    const uint32_t row = (t / kRegionTiles) * 8u + ((i >> 3) & 7u), col = (t % kRegionTiles) * 8u + (i & 7u);
-    const uint32_t x = (region % regions_x) * kRegion + col, y = (region / regions_x) * kRegion + row;
-    uint32_t c = 0u;
-    if (x < width && y < rows) c = min((uint32_t)rays[(size_t)y * width + x], 0x7fffu) + 1u;
-    key[i] = (c << kBits) | (kRegionPixels - 1u - i);  // descending: costliest, then earliest in tile order
-    __syncthreads();
-    for (uint32_t size = 2u; size <= kRegionPixels; size <<= 1) {  // bitonic sort, descending
-        for (uint32_t stride = size >> 1; stride > 0u; stride >>= 1) {
-            const uint32_t j = i ^ stride;
-            if (j > i) {
-                const uint32_t a = key[i], b = key[j];
-                if ((a < b) == ((i & size) == 0u)) {
-                    key[i] = b;
-                    key[j] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    const uint32_t src = kRegionPixels - 1u - (key[i] & (kRegionPixels - 1u));
-    const uint32_t st = src >> 6;
-    perm[(size_t)region * kRegionPixels + i] =
-        (PermT)(((st / kRegionTiles) * 8u + ((src >> 3) & 7u)) * kRegion + (st % kRegionTiles) * 8u + (src & 7u));
-}
-
 __global__ void rand_init_kernel(uint32_t* state) {  // RandInit (Kernel.cu:160-164)
     if (threadIdx.x == 0 && blockIdx.x == 0) curand_init_state(1984ull, state);
 }
@@ -2014,26 +1952,18 @@ thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupa
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
-thread_local int g_pixel_sort = 1;                          // RT_TUNE_PIXEL_SORT
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
 // evicts the cache meanwhile (the buffers are freed when the last holder drops it; hipFree waits for the
 // device, so a launch still reading them completes first).
-// With RT_TUNE_PIXEL_SORT the plan also holds the per-pixel ray counts of the last launch and the pixel order
-// pixel_sort_kernel derives from them for the next one.
 struct TilePlan {
     uint32_t* cost = nullptr;
     uint32_t* order = nullptr;
-    uint16_t* rays = nullptr;  // per local pixel
-    dev::PermT* perm = nullptr;  // one entry per pixel of the frame's regions
-    std::atomic<bool> valid{false};       // an order has been planned (by an earlier launch on the same stream)
-    std::atomic<bool> perm_valid{false};  // a pixel order has been sorted (idem)
+    std::atomic<bool> valid{false};  // an order has been planned (by an earlier launch on the same stream)
     ~TilePlan() {
         if (cost) (void)hipFree(cost);
         if (order) (void)hipFree(order);
-        if (rays) (void)hipFree(rays);
-        if (perm) (void)hipFree(perm);
     }
 };
 struct PlanKey {
@@ -2041,16 +1971,14 @@ struct PlanKey {
     void* stream;
     uint32_t tiles_x, tiles;
     int kind;  // kernel family
-    uint32_t width, rows, region_log2;  // the pixel order is valid for one frame shape and region size
     bool operator<(const PlanKey& o) const {
-        return std::tie(kind, device, stream, tiles_x, tiles, width, rows, region_log2) <
-               std::tie(o.kind, o.device, o.stream, o.tiles_x, o.tiles, o.width, o.rows, o.region_log2);
+        if (kind != o.kind) return kind < o.kind;
+        if (device != o.device) return device < o.device;
+        if (stream != o.stream) return stream < o.stream;
+        if (tiles_x != o.tiles_x) return tiles_x < o.tiles_x;
+        return tiles < o.tiles;
     }
 };
-constexpr uint32_t regions_x_of(uint32_t width, uint32_t rl) { return (width + (1u << rl) - 1u) >> rl; }
-constexpr uint32_t regions_of(uint32_t width, uint32_t rows, uint32_t rl) {
-    return regions_x_of(width, rl) * ((rows + (1u << rl) - 1u) >> rl);
-}
 // Automatic kernel choice below 64 spp, by measurement.  Which of v3 (tile waves, longest-first order) and v4
 // (persistent, per-lane pixel queue) is faster there depends on the scene as much as on spp (config 2's scene
 // at 4 spp: v3 1.54 vs v4 1.77 ms; config 5's at 4 spp: 0.89 vs 0.65; config 3's at 8 spp: 14.1 vs 12.8,
@@ -2100,17 +2028,6 @@ int acquire_plan(const PlanKey& key, hipStream_t s, std::shared_ptr<TilePlan>* o
         if (rc == RT_OK) rc = hip_check(hipMalloc(&o, (size_t)key.tiles * 4), "rt_render: tile order allocation");
         p->order = (uint32_t*)o;
         if (rc == RT_OK) rc = hip_check(hipMemsetAsync(c, 0, (size_t)key.tiles * 4, s), "rt_render: tile cost reset");
-        void* ry = nullptr;
-        void* pm = nullptr;
-        if (rc == RT_OK) rc = hip_check(hipMalloc(&ry, (size_t)key.width * key.rows * 2), "rt_render: pixel ray counts");
-        p->rays = (uint16_t*)ry;
-        if (rc == RT_OK)
-            rc = hip_check(hipMalloc(&pm, ((size_t)regions_of(key.width, key.rows, key.region_log2) << (2 * key.region_log2)) *
-                                              sizeof(dev::PermT)),
-                           "rt_render: pixel order");
-        p->perm = (dev::PermT*)pm;
-        if (rc == RT_OK)
-            rc = hip_check(hipMemsetAsync(ry, 0, (size_t)key.width * key.rows * 2, s), "rt_render: pixel ray counts reset");
         if (rc != RT_OK) return rc;
         it = g_plans.emplace(key, std::move(p)).first;
     }
@@ -2231,15 +2148,6 @@ int rt_set_tuning(int key, int value) {
         }
         int prev = g_adaptive_order;
         g_adaptive_order = value;
-        return prev;
-    }
-    if (key == RT_TUNE_PIXEL_SORT) {
-        if (value < 0 || value > 1) {
-            set_error("rt_set_tuning: pixel sort must be 0 or 1");
-            return RT_ERR_INVALID_ARGUMENT;
-        }
-        int prev = g_pixel_sort;
-        g_pixel_sort = value;
         return prev;
     }
     if (key == RT_TUNE_TEXEL_LAYOUT) {
@@ -2497,19 +2405,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (V.kernel == 3 && g_adaptive_order && !g_tile_order) {
         int device = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
-        if (rc == RT_OK)
-        // pixel order regions: 32 × 32, or 16 × 16 when a multi-rank split hands this rank bands of < 32 rows
-        P.region_log2 = (T.num_ranks > 1 && T.band_rows < 32u) ? 4u : 5u;
-        if (rc == RT_OK)
-            rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles, V.kernel, a->width, T.local_rows, P.region_log2},
-                              s, &plan);
+        if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles, V.kernel}, s, &plan);
         if (rc != RT_OK) return rc;
         P.tile_cost = plan->cost;
         P.tile_order = plan->valid.load() ? plan->order : nullptr;
-        if (g_pixel_sort) {
-            P.pixel_rays = plan->rays;
-            P.pixel_perm = plan->perm_valid.load() ? plan->perm : nullptr;
-        }
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing) {
@@ -2527,17 +2426,6 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                            tiles);
         rc = hip_check(hipGetLastError(), "rt_render: plan kernel launch", RT_ERR_LAUNCH);
         if (rc == RT_OK) plan->valid.store(true);
-        if (rc == RT_OK && P.pixel_rays) {  // ... and renders each region's pixels in cost order
-            const uint32_t rl = P.region_log2, regions = regions_of(a->width, T.local_rows, rl);
-            if (rl == 5u)
-                hipLaunchKernelGGL(dev::pixel_sort_kernel<32>, dim3(regions), dim3(1024), 0, s, (const uint16_t*)plan->rays,
-                                   plan->perm, a->width, T.local_rows, regions_x_of(a->width, rl));
-            else
-                hipLaunchKernelGGL(dev::pixel_sort_kernel<16>, dim3(regions), dim3(256), 0, s, (const uint16_t*)plan->rays,
-                                   plan->perm, a->width, T.local_rows, regions_x_of(a->width, rl));
-            rc = hip_check(hipGetLastError(), "rt_render: pixel sort kernel launch", RT_ERR_LAUNCH);
-            if (rc == RT_OK) plan->perm_valid.store(true);
-        }
     }
     if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);
     if (g_timing) {

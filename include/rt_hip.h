@@ -310,13 +310,9 @@ int rt_last_variant(void);
 /*   RT_TUNE_TEXEL_LAYOUT: device bytes per texel of the images of later rt_scene_create calls: 3 (default,
  *   the reference's RGB8 layout, Texture.cuh:76: three byte gathers per lookup) or 4 (RGBA8-padded: one dword
  *   gather per lookup, 4/3 the memory).  The image does not depend on it. */
-/*   RT_TUNE_PIXEL_SORT: 1 (default, with RT_TUNE_ADAPTIVE_ORDER) = the v3 kernels record every pixel's ray
- *   count and the next launch on the same stream with the same frame shape renders each 16x16 region's pixels
- *   in cost order (the region's four waves take its 64 costliest pixels, the next 64, ...) instead of as four
- *   8x8 tiles, so a wave's pixels finish at similar times; 0 = 8x8 tiles.  The image does not depend on it. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
-                     RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_PIXEL_SORT = 7 };
+                     RT_TUNE_TEXEL_LAYOUT = 6 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

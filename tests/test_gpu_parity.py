@@ -476,61 +476,6 @@ def test_adaptive_tile_order_changes_schedule_not_pixels():
         lib().rt_set_tuning(5, prev if prev >= 0 else 1)
 
 
-@pytest.mark.parametrize("shape", [(320, 176, 8, 1), (100, 37, 16, 1), (136, 72, 4, 1), (200, 88, 4, 3),
-                                   (72, 104, 4, 2)])
-def test_pixel_sort_changes_schedule_not_pixels(shape):
-    """RT_TUNE_PIXEL_SORT: after a launch records every pixel's ray count, the next v3 launch on the stream renders
-    each region's pixels in cost order (32x32 regions of 16 waves; 16x16 for a rank of a 16-row band split)
-    instead of as 8x8 tiles.  Ragged tile grids (100x37: right-edge regions with fewer tile columns and a partial
-    bottom row) must lose no pixel; frames before and after the reordering equal the oracle's."""
-    w, h, spp, ranks = shape
-    cfg = scenes.CONFIGS["c2"].scaled(w, h, spp)
-    ds = DeviceScene(scenes.builtin(cfg.scene))
-    lib().rt_set_variant(3)
-    prev = lib().rt_set_tuning(7, 0)
-    try:
-        r = Renderer(cfg.width, cfg.height, band_rows=16, num_ranks=ranks, rank=ranks - 1)
-        r.render_init()
-        r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
-        torch.cuda.synchronize()
-        tiles = r.image().copy()
-        rays_tiles = int(r.counters[0])
-        lib().rt_set_tuning(7, 1)
-        for _ in range(3):  # the first launch records ray counts, the next ones render in cost order
-            r.counters.zero_()
-            r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
-            torch.cuda.synchronize()
-            np.testing.assert_array_equal(r.image(), tiles)
-            assert int(r.counters[0]) == rays_tiles
-        st = po.init_states(cfg.width, cfg.height)
-        ref, _, _ = po.render(po.OracleScene(scenes.builtin(cfg.scene)), cfg.width, cfg.height, cfg.spp, cfg.depth,
-                              cfg.inputs(), st)
-        np.testing.assert_array_equal(tiles, ref[r.rows])
-    finally:
-        lib().rt_set_tuning(7, prev if prev >= 0 else 1)
-
-
-def test_pixel_sort_advances_every_rng_state():
-    """With the pixel order active, every pixel's XORWOW state is still advanced exactly once per frame (two frames
-    with state write-back equal the oracle's two frames, states included)."""
-    cfg = scenes.CONFIGS["c2"].scaled(104, 40, 4)
-    ds = DeviceScene(scenes.builtin(cfg.scene))
-    lib().rt_set_variant(3)
-    lib().rt_set_tuning(7, 1)
-    r = Renderer(cfg.width, cfg.height, state_layout="curand")
-    r.render_init()
-    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)  # records ray counts
-    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
-    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
-    torch.cuda.synchronize()
-    sc = po.OracleScene(scenes.builtin(cfg.scene))
-    st = po.init_states(cfg.width, cfg.height)
-    po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
-    ref, _, _ = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)  # st advances in place
-    np.testing.assert_array_equal(r.image(), ref)
-    np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
-
-
 def _small_rects_scene():
     """48 small axis-aligned rectangles (0.3-0.8 units) scattered around the origin, Lambertian."""
     rng = np.random.default_rng(11)
