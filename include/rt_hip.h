@@ -302,7 +302,7 @@ int rt_last_variant(void);
 /*   RT_TUNE_PERSISTENT_WAVES: waves per SIMD of the persistent kernels' grid (0 = occupancy query, default;
  *   1..16). */
 /*   RT_TUNE_SAH_TRAVERSAL: cost of a node visit relative to a primitive test in the SAH leaf decision, ×10
- *   (1..1000, default 12), used by later rt_scene_create calls. */
+  *   (1..1000, default 16), used by later rt_scene_create calls. */
 /*   RT_TUNE_LDS_PAD: diagnostic, extra LDS bytes per wave of the v3/v4 kernels (occupancy experiments; 0).
  *   RT_TUNE_ADAPTIVE_ORDER: 1 (default) = the v3 kernels dispatch a frame's tiles longest-first, ordered by
  *   the per-tile wave lifetimes the previous launch on the same stream with the same tile grid measured;

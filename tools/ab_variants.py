@@ -14,7 +14,7 @@ ap.add_argument("--spp", type=int, default=0)
 ap.add_argument("--thresholds", default="40", help="regen thresholds to try for resumable variants (>= 8)")
 ap.add_argument("--leafmax", default="4", help="BVH leaf sizes to try (RT_TUNE_LEAF_MAX)")
 ap.add_argument("--pwaves", default="0", help="persistent grid waves/SIMD to try (RT_TUNE_PERSISTENT_WAVES)")
-ap.add_argument("--sah", default="12", help="SAH traversal costs x10 to try (RT_TUNE_SAH_TRAVERSAL)")
+ap.add_argument("--sah", default="16", help="SAH traversal costs x10 to try (RT_TUNE_SAH_TRAVERSAL)")
 ap.add_argument("--rng", default="xorwow", choices=("xorwow", "philox"))
 args = ap.parse_args()
 cfg = scenes.CONFIGS[args.config]
@@ -34,7 +34,7 @@ for lm in sorted({v[2] for v in variants}):
     lib().rt_set_tuning(3, lm[1])
     scenes_by_lm[lm] = DeviceScene(scenes.builtin(cfg.scene))
 lib().rt_set_tuning(1, 4)
-lib().rt_set_tuning(3, 12)
+lib().rt_set_tuning(3, 16)
 r = Renderer(cfg.width, cfg.height, rng=args.rng)
 r.render_init()
 inp = cfg.inputs()
