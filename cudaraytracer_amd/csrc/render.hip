@@ -1894,8 +1894,8 @@ using KernelFn = void (*)(const dev::KParams);
 //   0  v1: scratch stack, 32-bit references       — fallback for scenes beyond 16-bit references and deep BVHs
 //   1  v2: 64-thread resumable, 32-bit LDS stacks — fallback for scenes beyond 16-bit references
 //   2  v3: 15-word parking                        — spp/depth too large for compact parking
-//   3  v3: 13-word compact parking                — default for spp >= 32
-//   4  v4: persistent work queue, 64-B nodes      — default for spp < 32 (a compact-parking, 48-B-node,
+//   3  v3: 13-word compact parking                — automatic choice from 64 spp; below, timed against 4
+//   4  v4: persistent work queue, 64-B nodes      — timed against 3 below 64 spp (a compact-parking, 48-B-node,
 //         longest-first-ordered v4 measured slower on C2, C3 and C5: profiles/r02_ab_v3_v4compact_c2.txt,
 //         profiles/r02_configs_v345.txt)
 struct Variant {
