@@ -40,6 +40,9 @@
 namespace rt {
 
 constexpr int kLeafMax = 4;         // max primitives per leaf (2-bit count in the leaf reference)
+// Deepest BVH the compact v3 kernel holds at 8 waves per SIMD: 13 parked words × 256 B + (depth + 2) × 128 B of
+// 16-bit stack per wave must fit 160 KB / 32 waves = 5120 B (render.hip, rt_render's LDS sizing)
+constexpr uint32_t kOccupancyDepth = 12;
 extern thread_local int g_leaf_max;  // rt_set_tuning(RT_TUNE_LEAF_MAX): 1..kLeafMax, read by the BVH build
 extern thread_local int g_sah_traversal_x10;  // rt_set_tuning(RT_TUNE_SAH_TRAVERSAL): SAH node cost × 10
 extern thread_local int g_texel_bytes;  // rt_set_tuning(RT_TUNE_TEXEL_LAYOUT): device bytes per texel, 3 or 4

@@ -81,6 +81,7 @@ struct BuildPrim {
 
 struct Builder {
     int leaf_max = kLeafMax;
+    float traversal = 1.6f;  // SAH: node visit cost / primitive test cost
     std::vector<BuildPrim> prims;
     std::vector<int> order;  // final primitive order
     struct Node {
@@ -130,8 +131,7 @@ struct Builder {
         }
         Box all = range_box(b, e);
         float leaf_cost = all.area() * (float)n;
-        const float kTraversal = (float)g_sah_traversal_x10 / 10.0f;  // node visit cost / primitive test cost
-        if (!must_split && n <= leaf_max && best_cost + kTraversal * all.area() >= leaf_cost) return make_leaf(b, e);
+        if (!must_split && n <= leaf_max && best_cost + traversal * all.area() >= leaf_cost) return make_leaf(b, e);
         std::stable_sort(order.begin() + b, order.begin() + e, [&](int x, int y) {
             return prims[x].centroid[best_axis] < prims[y].centroid[best_axis];
         });
@@ -148,6 +148,8 @@ struct Builder {
     }
 
     void build_root() {
+        nodes.clear();
+        max_depth = 0;
         int n = (int)prims.size();
         order.resize(n);
         std::iota(order.begin(), order.end(), 0);
@@ -306,7 +308,24 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         p.src = (int)i;
         B.prims.push_back(p);
     }
+    B.traversal = (float)g_sah_traversal_x10 / 10.0f;
     B.build_root();
+    // Occupancy guard: a tree deeper than kOccupancyDepth costs the compact v3 kernel its 8th wave per SIMD (its
+    // LDS stack grows by 128 B per level; C2's tree at depth 13 renders 8 % slower than at 12,
+    // profiles/r02e_ab_sah.txt).  Dearer node visits make the SAH stop splitting earlier: retry with 1.5×, 2×,
+    // 3× the cost and keep the first tree that fits; if none does, the first tree stays.
+    if (B.max_depth > kOccupancyDepth && B.prims.size() > 1) {
+        const float base = B.traversal;
+        for (const float f : {1.5f, 2.0f, 3.0f}) {
+            Builder T = B;
+            T.traversal = base * f;
+            T.build_root();
+            if (T.max_depth <= kOccupancyDepth) {
+                B = std::move(T);
+                break;
+            }
+        }
+    }
     out->num_prims = (uint32_t)B.prims.size();
     out->num_nodes = (uint32_t)B.nodes.size();
     out->depth = B.max_depth;

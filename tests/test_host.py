@@ -126,6 +126,19 @@ def test_bvh_is_shallow_and_small_for_rtiow():
     assert nodes.nbytes + info.num_prims * 32 <= 48 * 1024  # LDS-stageable
 
 
+def test_bvh_depth_guard_keeps_eight_wave_occupancy():
+    """A cheap node-visit SAH cost makes RTIOW's tree 13 levels deep, one more than the compact v3 kernel's LDS
+    holds at 8 waves/SIMD: the builder retries with dearer visits until the tree fits (scene_build.cpp)."""
+    prev = lib().rt_set_tuning(3, 6)
+    try:
+        info, nodes, _, _ = _tables(scenes.builtin(scenes.SCENE_RTIOW))
+        assert info.depth <= 12 and info.num_prims == 488
+    finally:
+        lib().rt_set_tuning(3, prev)
+    info, _, _, _ = _tables(scenes.builtin(scenes.SCENE_RTIOW))  # the default tree fits as built
+    assert info.depth <= 12
+
+
 def test_inactive_hittables_are_dropped():
     s = scenes.builtin(scenes.SCENE_DEFAULT_WORLD)
     s.hittables[3].is_active = 0
