@@ -328,6 +328,41 @@ def test_philox_mode_estimates_the_same_image():
     assert not np.array_equal(rp1, rp)
 
 
+def _rgb(pos, cfg):
+    return pos.view(np.uint8).reshape(cfg.height, cfg.width, 4)[..., :3].astype(np.float64)
+
+
+def test_philox_mode_meets_the_psnr_contract():
+    """SURVEY.md §8(c) C3, perf mode: PSNR >= 30 dB against a 1024-spp reference at low resolution.  RTIOW at
+    64x36: the Philox image at 64 spp (measured 36.1 dB) against the parity mode (cuRAND XORWOW) at 1024 spp.  (The
+    kernel's Philox mode equals this oracle's bit for bit: tests/test_gpu_parity.py.)"""
+    ref_cfg = scenes.CONFIGS["c2"].scaled(64, 36, 1024)
+    cfg = scenes.CONFIGS["c2"].scaled(64, 36, 64)
+    sc = po.OracleScene(scenes.builtin(cfg.scene))
+    ref, _, _ = po.render(sc, ref_cfg.width, ref_cfg.height, ref_cfg.spp, ref_cfg.depth, ref_cfg.inputs(),
+                          po.init_states(ref_cfg.width, ref_cfg.height), threads=8)
+    ph, _, _ = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), None, philox=True, threads=8)
+    mse = ((_rgb(ref, ref_cfg) - _rgb(ph, cfg)) ** 2).mean()
+    assert 10 * math.log10(255.0 ** 2 / mse) >= 30.0
+
+
+def test_philox_mode_estimates_the_cornell_image():
+    """The Cornell box (config 3's scene, emissive, depth 16) at 64x64, 64 spp: per channel, the image mean of
+    (philox - xorwow) pre-gamma radiance within 3 standard errors (3 sigma; measured 1.3-1.5),
+    and the same path-length distribution (ray counts within 1 %).  Cornell at 1024 spp is itself too noisy for a
+    PSNR bound (21 dB between 256 and 1024 spp), hence the mean test."""
+    cfg = scenes.CONFIGS["c3"].scaled(64, 64, 64)
+    sc = po.OracleScene(scenes.builtin(cfg.scene))
+    _, rx, cx = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(),
+                          po.init_states(cfg.width, cfg.height), radiance=True, threads=8)
+    _, rp, cp = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), None, radiance=True,
+                          philox=True, threads=8)
+    d = (rp[..., :3].astype(np.float64) - rx[..., :3].astype(np.float64)).reshape(-1, 3)
+    se = d.std(axis=0) / math.sqrt(d.shape[0])
+    assert np.all(np.abs(d.mean(axis=0)) < 3 * se), (d.mean(axis=0), se)
+    assert abs(cp.rays / cx.rays - 1.0) < 0.01
+
+
 def test_sphere_uv_acos_atan2_are_accurate_and_ieee_signed():
     """GetSphereUV's acos / atan2 (fixed binary32 sequences shared by kernel and oracle, rt_oracle.c): within
     3 ulp of the double-precision functions, with IEEE atan2's signed-zero quadrants."""
