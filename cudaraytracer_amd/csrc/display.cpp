@@ -14,6 +14,7 @@
 #include <hip/hip_gl_interop.h>
 
 #include <cstdio>
+#include <exception>
 #include <new>
 #include <cstring>
 #include <string>
@@ -48,8 +49,15 @@ int rt_write_ppm(const char* path, const uint32_t* rgba, uint32_t width, uint32_
         rt::set_error(std::string("rt_write_ppm: cannot open ") + path);
         return RT_ERR_INVALID_ARGUMENT;
     }
+    std::vector<uint8_t> row;
+    try {
+        row.resize((size_t)width * 3);
+    } catch (const std::exception&) {  // nothing may throw through the C ABI
+        std::fclose(f);
+        rt::set_error("rt_write_ppm: host allocation failed");
+        return RT_ERR_OUT_OF_MEMORY;
+    }
     std::fprintf(f, "P6\n%u %u\n255\n", width, height);
-    std::vector<uint8_t> row((size_t)width * 3);
     bool ok = true;
     for (uint32_t y = 0; y < height && ok; y++) {
         // PPM rows run top to bottom; the framebuffer's row 0 is the bottom of the image (Kernel.cu:157)
@@ -85,7 +93,13 @@ int rt_copy_image_to_host(uint32_t* host, const uint32_t* device_pos, uint32_t w
     rc = hip_status(hipStreamSynchronize(s), "rt_copy_image_to_host: hipStreamSynchronize");
     if (rc || !flip_rows) return rc;
     // top row first, as glTexSubImage2D with a top-left origin or an image file expects (CudaLayer.cpp:402)
-    std::vector<uint32_t> tmp(width);
+    std::vector<uint32_t> tmp;
+    try {
+        tmp.resize(width);
+    } catch (const std::exception&) {
+        rt::set_error("rt_copy_image_to_host: host allocation failed");
+        return RT_ERR_OUT_OF_MEMORY;
+    }
     for (uint32_t y = 0; y < height / 2; y++) {
         uint32_t* a = host + (size_t)y * width;
         uint32_t* b = host + (size_t)(height - 1 - y) * width;

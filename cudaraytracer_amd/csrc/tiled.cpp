@@ -170,12 +170,23 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
         dst_device = attr.device;
     }
     const uint32_t frame = f->rng_frame_set ? f->rng_frame : t->frame;
+    // An error after some ranks have been launched returns only once their streams are idle: the caller may
+    // free `pos` (or the scene) as soon as the call fails, and an in-flight render or gather would write into it.
+    auto drain = [t](int rc) {
+        std::string msg = rt_last_error();
+        for (rt_tiled::Rank& k : t->ranks)
+            if (k.stream && hipSetDevice(k.device) == hipSuccess) (void)hipStreamSynchronize(k.stream);
+        (void)hipGetLastError();
+        set_error(msg);
+        return rc;
+    };
     // 1. every rank renders its bands on its own stream (concurrently)
     for (uint32_t r = 0; r < N; r++) {
         rt_tiled::Rank& k = t->ranks[r];
-        if (int rc = hip_err(hipSetDevice(k.device), "hipSetDevice")) return rc;
-        if (int rc = hip_err(hipEventRecord(k.ev[0], k.stream), "hipEventRecord")) return rc;
-        if (int rc = hip_err(hipMemsetAsync(k.counters, 0, 16 * sizeof(uint64_t), k.stream), "counter reset")) return rc;
+        if (int rc = hip_err(hipSetDevice(k.device), "hipSetDevice")) return drain(rc);
+        if (int rc = hip_err(hipEventRecord(k.ev[0], k.stream), "hipEventRecord")) return drain(rc);
+        if (int rc = hip_err(hipMemsetAsync(k.counters, 0, 16 * sizeof(uint64_t), k.stream), "counter reset"))
+            return drain(rc);
         if (k.local_rows) {
             rt_render_args a{};
             a.pos = k.pos;
@@ -191,9 +202,9 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
             a.inputs = f->inputs;
             a.rng_seed = t->desc.seed;
             a.rng_frame = frame;
-            if (int rc = rt_render(t->scenes[k.device], &a, k.stream)) return rc;
+            if (int rc = rt_render(t->scenes[k.device], &a, k.stream)) return drain(rc);
         }
-        if (int rc = hip_err(hipEventRecord(k.ev[1], k.stream), "hipEventRecord")) return rc;
+        if (int rc = hip_err(hipEventRecord(k.ev[1], k.stream), "hipEventRecord")) return drain(rc);
     }
     // 2. gather + unshuffle: rank r's local band k → global band k·N + r of the destination frame, one
     //    strided 2-D copy per rank over the peer link (the last global band may be partial: copied apart)
@@ -205,7 +216,7 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
             if (hipDeviceCanAccessPeer(&can, k.device, dst_device) == hipSuccess && can) {
                 const hipError_t e = hipDeviceEnablePeerAccess(dst_device, 0);
                 if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-                    return hip_err(e, "hipDeviceEnablePeerAccess");
+                    return drain(hip_err(e, "hipDeviceEnablePeerAccess"));
                 (void)hipGetLastError();
             }
         }
@@ -217,7 +228,7 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
                 if (int rc = hip_err(hipMemcpy2DAsync(dst0, band_bytes * N, k.pos, band_bytes, band_bytes, full,
                                                       hipMemcpyDefault, k.stream),
                                      "gather (hipMemcpy2DAsync)"))
-                    return rc;
+                    return drain(rc);
             }
             const uint32_t tail = k.local_rows - full * B;
             if (tail) {
@@ -225,24 +236,25 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
                 if (int rc = hip_err(hipMemcpyAsync(dst, k.pos + (size_t)full * B * W, (size_t)tail * W * 4,
                                                     hipMemcpyDefault, k.stream),
                                      "gather (hipMemcpyAsync)"))
-                    return rc;
+                    return drain(rc);
             }
         }
-        if (int rc = hip_err(hipEventRecord(k.ev[2], k.stream), "hipEventRecord")) return rc;
+        if (int rc = hip_err(hipEventRecord(k.ev[2], k.stream), "hipEventRecord")) return drain(rc);
     }
     // 3. wait for every rank (the call is synchronous, as LaunchKernel is, Kernel.cu:190)
     float render_ms = 0.0f, gather_ms = 0.0f;
     uint64_t rays = 0;
     for (rt_tiled::Rank& k : t->ranks) {
         (void)hipSetDevice(k.device);
-        if (int rc = hip_err(hipStreamSynchronize(k.stream), "hipStreamSynchronize")) return rc;
+        if (int rc = hip_err(hipStreamSynchronize(k.stream), "hipStreamSynchronize")) return drain(rc);
         float a = 0.0f, b = 0.0f;
         (void)hipEventElapsedTime(&a, k.ev[0], k.ev[1]);
         (void)hipEventElapsedTime(&b, k.ev[1], k.ev[2]);
         render_ms = std::max(render_ms, a);
         gather_ms = std::max(gather_ms, b);
         uint64_t c = 0;
-        if (int rc = hip_err(hipMemcpy(&c, k.counters, sizeof(c), hipMemcpyDeviceToHost), "counter readback")) return rc;
+        if (int rc = hip_err(hipMemcpy(&c, k.counters, sizeof(c), hipMemcpyDeviceToHost), "counter readback"))
+            return drain(rc);
         rays += c;
     }
     if (!f->rng_frame_set && !(f->flags & RT_FLAG_NO_STATE_WRITEBACK)) t->frame++;
