@@ -1261,6 +1261,7 @@ __device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col,
 typedef const __attribute__((address_space(4))) float ConstF32;
 typedef const __attribute__((address_space(4))) uint32_t ConstU32;
 typedef const __attribute__((address_space(4))) uint8_t ConstU8;
+typedef __attribute__((address_space(3))) uint16_t LdsU16;
 #ifndef RT_DIAG_NONE
 #define RT_DIAG_NONE 0
 #endif
@@ -1284,7 +1285,7 @@ constexpr bool kScalarNodes = RT_SCALAR_NODES != 0;
 // Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
 // until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
 // still tracing (the wave then shades the finished lanes and regenerates them).
-template <bool COUNT_TESTS, int NODES>
+template <bool COUNT_TESTS, int NODES, uint32_t STK_OFF>
 __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, const __amdgpu_buffer_rsrc_t rrsrc,
                                             const float4* __restrict__ nodes_tab, const uint32_t* __restrict__ refs16,
                                             const float4* __restrict__ prims, int16_t* const stk,
@@ -1310,6 +1311,10 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     const f3 pa = mk(fmaxf(invd.x, 0.0f), fmaxf(invd.y, 0.0f), fmaxf(invd.z, 0.0f));
     const f3 pc = mk(fminf(invd.x, 0.0f), fminf(invd.y, 0.0f), fminf(invd.z, 0.0f));
     const uint16_t* ustk = (const uint16_t*)stk;
+    // LDS address of this lane's stack entry 0 split into the lane part (VGPR) and the stack region's offset
+    // STK_OFF (an immediate of the ds instructions)
+    const uint32_t stk_lane = (uint32_t)(uintptr_t)(LdsU16*)stk - STK_OFF;  // LDS base + the lane's 2-byte column
+    constexpr uint32_t stk_off = STK_OFF / 2;  // in uint16 units
     const float tmin_s = kTmin;  // an SGPR operand of the slab test's v_max
 #if RT_PRIM_BUFFER
     const __amdgpu_buffer_rsrc_t prsrc = __builtin_amdgcn_make_buffer_rsrc((void*)prims, (short)0, 0x7fffffff, 0x00020000);
@@ -1320,8 +1325,13 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         const uint32_t n_outer = COUNT_TESTS ? (uint32_t)__popcll(__ballot(1)) : 0u;  // lanes still tracing
         (void)n_outer;
         while (node < (uint32_t)kSentinel16) {
-            uint32_t top1 = ustk[(sp - 1u) * 64];
-            uint32_t top2 = ustk[(sp - 2u) * 64];
+            // the entry address as one v_lshl_add_u32 (LLVM emits a half-rate shift plus an add: C2 −0.2 %,
+            // C3 −0.3 %, profiles/r02e_ab_stack_addr.txt)
+            uint32_t sa;
+            asm("v_lshl_add_u32 %0, %1, 7, %2" : "=v"(sa) : "v"(sp), "v"(stk_lane));
+            LdsU16* const sp_entry = (LdsU16*)(uintptr_t)sa + stk_off;
+            uint32_t top1 = sp_entry[-64];
+            uint32_t top2 = sp_entry[-128];
             // materialise the zero-extended words here: used in another basic block, the loaded u16 would
             // otherwise be re-extended there with a v_and per word and visit
             asm("" : "+v"(top1));
@@ -1425,7 +1435,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             const bool both = h0 && h1, none = !(h0 || h1);
             const uint32_t nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
             const uint32_t farc = swap ? ch0 : ch1;
-            stk[sp * 64] = (int16_t)farc;
+            *sp_entry = (uint16_t)farc;
             uint32_t nxt = none ? top1 : nearc;
             // no underflow guards: the two sentinel pads below kStackBase make a pop of the empty stack
             // yield kSentinel16, which ends this lane's traversal before sp can drop further
@@ -1583,7 +1593,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt, ntrav);
+            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt, ntrav);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -1689,7 +1699,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     const uint32_t threshold = P.regen_threshold;
 
     while (true) {
-        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
         uint32_t sample, depth, rays;
