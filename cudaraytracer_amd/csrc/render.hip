@@ -1314,6 +1314,11 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     // LDS address of this lane's stack entry 0 split into the lane part (VGPR) and the stack region's offset
     // STK_OFF (an immediate of the ds instructions)
     const uint32_t stk_lane = (uint32_t)(uintptr_t)(LdsU16*)stk - STK_OFF;  // LDS base + the lane's 2-byte column
+    // structured (stride 48 B / 4 B) views of the node boxes and references for the vector path's idxen loads
+    const __amdgpu_buffer_rsrc_t rsrc_nodes_idx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)nodes_tab, (short)48, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc_refs_idx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)refs16, (short)4, 0x7fffffff, 0x00020000);
     constexpr uint32_t stk_off = STK_OFF / 2;  // in uint16 units
     const float tmin_s = kTmin;  // an SGPR operand of the slab test's v_max
 #if RT_PRIM_BUFFER
@@ -1397,14 +1402,22 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     slab(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
                          make_float4(cn[8], cn[9], cn[10], cn[11]));
                 } else {
-                    uint32_t noff;  // node · 48 with the full-rate 24-bit multiply (LLVM otherwise emits v_mul_lo_u32)
-                    asm("v_mul_u32_u24 %0, 48, %1" : "=v"(noff) : "v"(node));
-                    const uint32_t refs = __builtin_amdgcn_raw_buffer_load_b32(rrsrc, (uint32_t)node * 4u, 0, 0);
+                    // structured buffer loads: the descriptors' strides (48 B, 4 B) scale the node index in the
+                    // addresser, no VALU offset arithmetic (C2 −0.5 %, profiles/r02e_ab_idxen.txt); the builtins have no idxen form, so the four loads
+                    // and their wait are one asm block
+                    uint32_t refs;
+                    float4 n0, n1, n2;
+                    asm volatile(
+                        "buffer_load_dword %0, %4, %5, 0 idxen\n\t"
+                        "buffer_load_dwordx4 %1, %4, %6, 0 idxen\n\t"
+                        "buffer_load_dwordx4 %2, %4, %6, 0 idxen offset:16\n\t"
+                        "buffer_load_dwordx4 %3, %4, %6, 0 idxen offset:32\n\t"
+                        "s_waitcnt vmcnt(0)"
+                        : "=&v"(refs), "=&v"(n0), "=&v"(n1), "=&v"(n2)
+                        : "v"(node), "s"(rsrc_refs_idx), "s"(rsrc_nodes_idx));
                     ch0 = refs & 0xffffu;
                     ch1 = refs >> 16;
-                    slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
-                         __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
+                    slab(n0, n1, n2);
                 }
             }
             if (COUNT_TESTS) {
