@@ -1314,11 +1314,9 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     // LDS address of this lane's stack entry 0 split into the lane part (VGPR) and the stack region's offset
     // STK_OFF (an immediate of the ds instructions)
     const uint32_t stk_lane = (uint32_t)(uintptr_t)(LdsU16*)stk - STK_OFF;  // LDS base + the lane's 2-byte column
-    // structured (stride 48 B / 4 B) views of the node boxes and references for the vector path's idxen loads
+    // structured (stride 48 B) view of the node boxes for the vector path's idxen loads
     const __amdgpu_buffer_rsrc_t rsrc_nodes_idx =
         __builtin_amdgcn_make_buffer_rsrc((void*)nodes_tab, (short)48, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsrc_refs_idx =
-        __builtin_amdgcn_make_buffer_rsrc((void*)refs16, (short)4, 0x7fffffff, 0x00020000);
     constexpr uint32_t stk_off = STK_OFF / 2;  // in uint16 units
     const float tmin_s = kTmin;  // an SGPR operand of the slab test's v_max
 #if RT_PRIM_BUFFER
@@ -1402,21 +1400,24 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     slab(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
                          make_float4(cn[8], cn[9], cn[10], cn[11]));
                 } else {
-                    // structured buffer loads: the descriptors' strides (48 B, 4 B) scale the node index in the
-                    // addresser, no VALU offset arithmetic (C2 −0.5 %, profiles/r02e_ab_idxen.txt); the builtins have no idxen form, so the four loads
-                    // and their wait are one asm block
-                    uint32_t refs;
+                    // Three structured (idxen) buffer loads: the descriptor's 48-B stride scales the node index in
+                    // the addresser (no VALU offset arithmetic: C2 −0.5 %), and the child references ride in the low
+                    // bytes of the x planes (scene_build.cpp), so no fourth load (C2 −1.6 %: the texture addresser
+                    // limits this loop as much as the VALU does — a fifth load costs +6.6 %;
+                    // profiles/r02e_ab_idxen.txt, profiles/r02e_ab_node_loads.txt).  The builtins have no idxen form:
+                    // the loads and their wait are one asm block.
                     float4 n0, n1, n2;
                     asm volatile(
-                        "buffer_load_dword %0, %4, %5, 0 idxen\n\t"
-                        "buffer_load_dwordx4 %1, %4, %6, 0 idxen\n\t"
-                        "buffer_load_dwordx4 %2, %4, %6, 0 idxen offset:16\n\t"
-                        "buffer_load_dwordx4 %3, %4, %6, 0 idxen offset:32\n\t"
+                        "buffer_load_dwordx4 %0, %3, %4, 0 idxen\n\t"
+                        "buffer_load_dwordx4 %1, %3, %4, 0 idxen offset:16\n\t"
+                        "buffer_load_dwordx4 %2, %3, %4, 0 idxen offset:32\n\t"
                         "s_waitcnt vmcnt(0)"
-                        : "=&v"(refs), "=&v"(n0), "=&v"(n1), "=&v"(n2)
-                        : "v"(node), "s"(rsrc_refs_idx), "s"(rsrc_nodes_idx));
-                    ch0 = refs & 0xffffu;
-                    ch1 = refs >> 16;
+                        : "=&v"(n0), "=&v"(n1), "=&v"(n2)
+                        : "v"(node), "s"(rsrc_nodes_idx));
+                    // byte 0 of lo_x | byte 0 of hi_x << 8 (v_perm: bytes 0-3 = src1, 4-7 = src0, 0x0c = zero)
+                    // (a VOP3 takes no literal on gfx9: the selector is an SGPR operand)
+                    asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch0) : "v"(n0.y), "v"(n0.x), "s"(0x0c0c0400u));
+                    asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch1) : "v"(n1.y), "v"(n1.x), "s"(0x0c0c0400u));
                     slab(n0, n1, n2);
                 }
             }

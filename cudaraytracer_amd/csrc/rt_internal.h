@@ -50,7 +50,8 @@ constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) trave
 
 struct HostScene {
     std::vector<float> nodes;   // 16 floats per node
-    std::vector<float> nodes48; // 12 floats per node: the three box float4 of `nodes` (v3 kernels)
+    std::vector<float> nodes48; // 12 floats per node: the three box float4 of `nodes` (v3 kernels), each child
+                                // reference also in the low bytes of its x planes (moved outward; scene_build.cpp)
     std::vector<uint32_t> refs16;  // per node: child 0 | child 1 << 16 as signed 16-bit references
     std::vector<float> prims;   // 8 floats per primitive
     std::vector<float> mats;    // 12 floats per material

@@ -73,6 +73,27 @@ Box prim_box(const rt_hittable_desc& h) {
     return b;
 }
 
+// v with the low byte of its binary32 representation replaced by `payload`, moved outward: the result is <= v
+// (up = false) or >= v (up = true).  Works on the magnitude, whose bit pattern orders like the value; a zero
+// or tiny magnitude crosses to the other sign's side (a denormal of the right sign).
+float with_low_byte(float v, uint32_t payload, bool up) {
+    uint32_t b;
+    std::memcpy(&b, &v, 4);
+    const uint32_t sign = b & 0x80000000u, mag = b & 0x7fffffffu;
+    const bool grow = (sign == 0) == up;  // the magnitude must not shrink (else: must not grow)
+    uint32_t out;
+    if (grow) {
+        out = sign | (((mag >> 8) + 1u) << 8) | payload;  // > mag
+    } else if ((mag >> 8) > 0u) {
+        out = sign | (((mag >> 8) - 1u) << 8) | payload;  // < mag
+    } else {
+        out = (sign ^ 0x80000000u) | 0x100u | payload;  // |v| < 256 ulps of 2^-149: a denormal past zero
+    }
+    float r;
+    std::memcpy(&r, &out, 4);
+    return r;
+}
+
 struct BuildPrim {
     Box box;
     float centroid[3];
@@ -345,9 +366,19 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
     out->nodes48.resize((size_t)out->num_nodes * 12);
     out->refs16.resize(out->num_nodes);
     for (uint32_t i = 0; i < out->num_nodes; i++) {
-        for (int k = 0; k < 12; k++) out->nodes48[(size_t)i * 12 + k] = out->nodes[(size_t)i * 16 + k];
+        float* o48 = out->nodes48.data() + (size_t)i * 12;
+        for (int k = 0; k < 12; k++) o48[k] = out->nodes[(size_t)i * 16 + k];
         const Builder::Node& n = B.nodes[i];
-        out->refs16[i] = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);  // valid when refs fit int16
+        const uint32_t r = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);  // valid when refs fit int16
+        out->refs16[i] = r;
+        // The two 16-bit child references also ride in the low bytes of the x planes (lo_x, hi_x of each child),
+        // so a lane's three 16-B box loads carry them and the vector path needs no fourth load (render.hip).
+        // Each carrier plane moves outward by < 512 ulps (lo down, hi up): the box only grows, and the culling
+        // stays conservative.
+        o48[0] = with_low_byte(o48[0], r & 0xffu, false);
+        o48[1] = with_low_byte(o48[1], (r >> 8) & 0xffu, true);
+        o48[4] = with_low_byte(o48[4], (r >> 16) & 0xffu, false);
+        o48[5] = with_low_byte(o48[5], r >> 24, true);
     }
     out->prims.resize((size_t)out->num_prims * 8);
     out->prim_source.resize(out->num_prims);

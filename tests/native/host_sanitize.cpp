@@ -4,6 +4,7 @@
 // Built and run by `make -C cudaraytracer_amd/csrc asan` (tests/test_sanitize.py); no GPU is needed: the
 // device calls fail cleanly and must come back as status codes.  Exit status 0 = every check held and the
 // sanitizers reported nothing (they abort the process on the first report).
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -12,6 +13,7 @@
 
 #include "../../include/rt_hip.h"
 #include "../../include/rt_reference_graph.h"
+#include "../../cudaraytracer_amd/csrc/rt_internal.h"
 
 static int failures = 0;
 #define CHECK(cond)                                                                  \
@@ -233,7 +235,46 @@ static void outputs_and_misc() {
     CHECK(rt_gl_register_texture(0, 0x0DE1, nullptr) == RT_ERR_INVALID_ARGUMENT);
 }
 
+// The v3 node table carries each node's two 16-bit child references in the low bytes of its x planes
+// (scene_build.cpp, render.hip's vector path): the decoded references equal refs16, and every carrier plane
+// moved outward (lo down, hi up) by under 512 ulps, so the boxes only grew.
+static void node_reference_payload() {
+    uint32_t checked = 0;
+    for (int which = 0; which < 6; which++) {
+        uint32_t nh = 0, nm = 0;
+        if (rt_builtin_scene(which, 1, nullptr, &nh, nullptr, &nm) != RT_OK) continue;
+        std::vector<rt_hittable_desc> h(nh);
+        std::vector<rt_material_desc> m(nm);
+        CHECK(rt_builtin_scene(which, 1, h.data(), &nh, m.data(), &nm) == RT_OK);
+        rt_scene_desc d{};
+        d.hittables = h.data();
+        d.num_hittables = nh;
+        d.materials = m.data();
+        d.num_materials = nm;
+        rt::HostScene hs;
+        std::string err;
+        if (rt::build_host_scene(&d, &hs, &err, false) != RT_OK) continue;  // scenes needing images
+        for (uint32_t i = 0; i < hs.num_nodes; i++) {
+            const float* o = hs.nodes.data() + (size_t)i * 16;
+            const float* q = hs.nodes48.data() + (size_t)i * 12;
+            uint32_t b[4];
+            std::memcpy(&b[0], &q[0], 4);
+            std::memcpy(&b[1], &q[1], 4);
+            std::memcpy(&b[2], &q[4], 4);
+            std::memcpy(&b[3], &q[5], 4);
+            const uint32_t r = (b[0] & 0xffu) | ((b[1] & 0xffu) << 8) | ((b[2] & 0xffu) << 16) | ((b[3] & 0xffu) << 24);
+            CHECK(r == hs.refs16[i]);
+            for (int k : {0, 4}) CHECK(q[k] <= o[k] && o[k] - q[k] <= 512.0f * std::fabs(o[k]) * 0x1p-23f + 0x1p-140f);
+            for (int k : {1, 5}) CHECK(q[k] >= o[k] && q[k] - o[k] <= 512.0f * std::fabs(o[k]) * 0x1p-23f + 0x1p-140f);
+            for (int k : {2, 3, 6, 7, 8, 9, 10, 11}) CHECK(q[k] == o[k]);
+            checked++;
+        }
+    }
+    CHECK(checked > 250);  // RTIOW alone has 286 nodes
+}
+
 int main() {
+    node_reference_payload();
     builtin_scenes();
     invalid_scenes();
     reference_graph();
