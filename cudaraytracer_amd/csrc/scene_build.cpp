@@ -82,6 +82,7 @@ float with_low_byte(float v, uint32_t payload, bool up) {
     const uint32_t sign = b & 0x80000000u, mag = b & 0x7fffffffu;
     const bool grow = (sign == 0) == up;  // the magnitude must not shrink (else: must not grow)
     uint32_t out;
+    // (a plane at the float range's end keeps its magnitude just under FLT_MAX: no finite ray reaches past it)
     if (grow) {
         out = sign | (((mag >> 8) + 1u) << 8) | payload;  // > mag
     } else if ((mag >> 8) > 0u) {
@@ -89,6 +90,7 @@ float with_low_byte(float v, uint32_t payload, bool up) {
     } else {
         out = (sign ^ 0x80000000u) | 0x100u | payload;  // |v| < 256 ulps of 2^-149: a denormal past zero
     }
+    if ((out & 0x7fffffffu) >= 0x7f7fff00u) out = (out & 0x80000000u) | 0x7f7fff00u | payload;  // stay finite
     float r;
     std::memcpy(&r, &out, 4);
     return r;
@@ -153,6 +155,10 @@ struct Builder {
         Box all = range_box(b, e);
         float leaf_cost = all.area() * (float)n;
         if (!must_split && n <= leaf_max && best_cost + traversal * all.area() >= leaf_cost) return make_leaf(b, e);
+        if (best_axis < 0) {  // every candidate cost overflowed (boxes at the end of the float range): object median
+            best_axis = 0;
+            best_split = n / 2;
+        }
         std::stable_sort(order.begin() + b, order.begin() + e, [&](int x, int y) {
             return prims[x].centroid[best_axis] < prims[y].centroid[best_axis];
         });
@@ -321,6 +327,13 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         if (h.material < 0 || (uint32_t)h.material >= desc->num_materials) {
             *err = "hittable " + std::to_string(i) + ": material index " + std::to_string(h.material) +
                    " out of range";
+            return RT_ERR_INVALID_SCENE;
+        }
+        // NaN or infinite geometry has no box (the reference's own AABB would poison every ancestor box)
+        const bool sphere = h.type == RT_SPHERE;
+        if (!std::isfinite(h.center[0]) || !std::isfinite(h.center[1]) || !std::isfinite(h.center[2]) ||
+            (sphere ? !std::isfinite(h.radius) : (!std::isfinite(h.width) || !std::isfinite(h.height)))) {
+            *err = "hittable " + std::to_string(i) + ": non-finite centre or size";
             return RT_ERR_INVALID_SCENE;
         }
         BuildPrim p;

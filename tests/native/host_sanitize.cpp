@@ -271,6 +271,30 @@ static void node_reference_payload() {
         }
     }
     CHECK(checked > 250);  // RTIOW alone has 286 nodes
+    // a box at the end of the float range: carrier planes stay finite
+    rt_material_desc m{};
+    m.type = RT_LAMBERTIAN;
+    m.albedo.type = RT_CONSTANT;
+    m.albedo.image = -1;
+    rt_hittable_desc h[2] = {};
+    for (int k = 0; k < 2; k++) {
+        h[k].type = RT_SPHERE;
+        h[k].is_active = 1;
+        h[k].center[0] = k ? 3.0e38f : -3.0e38f;
+        h[k].radius = 3.0e38f;
+    }
+    rt_scene_desc d{};
+    d.hittables = h;
+    d.num_hittables = 2;
+    d.materials = &m;
+    d.num_materials = 1;
+    rt::HostScene hs;
+    std::string err;
+    CHECK(rt::build_host_scene(&d, &hs, &err, false) == RT_OK);
+    for (float v : hs.nodes48) CHECK(!std::isnan(v));
+    // NaN geometry is rejected
+    h[1].center[1] = std::nanf("");
+    CHECK(rt::build_host_scene(&d, &hs, &err, false) == RT_ERR_INVALID_SCENE);
 }
 
 int main() {
