@@ -1262,6 +1262,12 @@ typedef const __attribute__((address_space(4))) float ConstF32;
 typedef const __attribute__((address_space(4))) uint32_t ConstU32;
 typedef const __attribute__((address_space(4))) uint8_t ConstU8;
 typedef __attribute__((address_space(3))) uint16_t LdsU16;
+// Visit decision of the v3/v4 node loop: 2 = inline-asm lane-mask block with the "no leaf held" mask carried
+// in SGPRs through the visits (default: C2 −0.7 %, profiles/r02h_ab_asm_decide.txt), 1 = the same block with a
+// per-visit compare of `leaf`, 0 = the C++ statement of the decision (the specification of both)
+#ifndef RT_ASM_DECIDE
+#define RT_ASM_DECIDE 2
+#endif
 #ifndef RT_DIAG_NONE
 #define RT_DIAG_NONE 0
 #endif
@@ -1327,6 +1333,10 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         const float t_best_c = __builtin_canonicalizef(t_best);
         const uint32_t n_outer = COUNT_TESTS ? (uint32_t)__popcll(__ballot(1)) : 0u;  // lanes still tracing
         (void)n_outer;
+#if RT_ASM_DECIDE
+        // lanes holding no leaf yet (RT_ASM_DECIDE >= 2 carries it through the visits as an SGPR mask)
+        uint64_t lzm = __ballot(leaf == 0);
+#endif
         while (node < (uint32_t)kSentinel16) {
             // the entry address as one v_lshl_add_u32 (LLVM emits a half-rate shift plus an add: C2 −0.2 %,
             // C3 −0.3 %, profiles/r02e_ab_stack_addr.txt)
@@ -1443,6 +1453,55 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 }
 #endif
             }
+#if RT_ASM_DECIDE
+            // The visit decision as one block of lane-mask arithmetic: the hit / order / leaf masks stay in SGPR
+            // pairs (SALU combines them), one compare of `leaf` serves both the postpone decision and the exit
+            // mask, and the exit test needs no VALU materialisation of a ballot.  Same results as the C++ below.
+            {
+                uint32_t farc, xr, nxt, at;
+                uint64_t m0, m1, m2, m3, m4, m5;
+                asm volatile(
+                    "v_cmp_le_f32 %[m0], %[a0], %[b0]\n\t"            // h0
+                    "v_cmp_le_f32 %[m1], %[a1], %[b1]\n\t"            // h1
+                    "v_cmp_lt_f32 %[m2], %[a1], %[a0]\n\t"            // swap
+                    "v_cndmask_b32 %[farc], %[ch1], %[ch0], %[m2]\n\t" // far child = swap ? ch0 : ch1
+                    "s_orn2_b64 %[m2], %[m2], %[m0]\n\t"              // swap | !h0
+                    "s_and_b64 %[m2], %[m2], %[m1]\n\t"               // take ch1 first
+                    "v_cndmask_b32 %[xr], %[ch0], %[ch1], %[m2]\n\t"
+                    "s_and_b64 %[m2], %[m0], %[m1]\n\t"               // both
+                    "s_or_b64 %[m0], %[m0], %[m1]\n\t"                // any
+                    "v_cndmask_b32 %[nxt], %[t1], %[xr], %[m0]\n\t"    // next = any ? first : pop
+                    "v_cndmask_b32 %[at], %[t2], %[t1], %[m0]\n\t"     // the stack top after this visit
+                    "v_cndmask_b32 %[at], %[at], %[farc], %[m2]\n\t"
+                    "v_addc_co_u32 %[sp], %[m3], %[sp], 0, %[m2]\n\t"  // push
+                    "s_not_b64 %[m0], %[m0]\n\t"                      // none
+                    "v_subb_co_u32 %[sp], %[m3], %[sp], 0, %[m0]\n\t"  // pop
+                    "v_cmp_lt_u32 %[m1], %[sent], %[nxt]\n\t"         // next is a leaf
+#if RT_ASM_DECIDE >= 2
+                    "s_mov_b64 %[m4], %[lzm]\n\t"                     // no leaf held yet (carried mask)
+#else
+                    "v_cmp_eq_u32 %[m4], 0, %[leaf]\n\t"              // no leaf held yet
+#endif
+                    "s_and_b64 %[m1], %[m1], %[m4]\n\t"               // postpone
+                    "v_cndmask_b32 %[leaf], %[leaf], %[nxt], %[m1]\n\t"
+                    "v_cndmask_b32 %[node], %[nxt], %[at], %[m1]\n\t"
+                    "v_subb_co_u32 %[sp], %[m3], %[sp], 0, %[m1]\n\t"  // pop the entry under the postponed leaf
+                    "s_andn2_b64 %[m5], %[m4], %[m1]\n\t"             // lanes still without a leaf
+#if RT_ASM_DECIDE >= 2
+                    "s_mov_b64 %[lzm], %[m5]\n\t"
+#endif
+                    "s_and_b64 %[m5], %[m5], exec"
+                    : [farc] "=&v"(farc), [xr] "=&v"(xr), [nxt] "=&v"(nxt), [at] "=&v"(at), [node] "=&v"(node),
+                      [sp] "+v"(sp), [leaf] "+v"(leaf), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
+                      [m3] "=&s"(m3), [m4] "=&s"(m4), [m5] "=&s"(m5), [lzm] "+s"(lzm)
+                    : [a0] "v"(c0min), [b0] "v"(c0max), [a1] "v"(c1min), [b1] "v"(c1max), [ch0] "v"(ch0),
+                      [ch1] "v"(ch1), [t1] "v"(top1), [t2] "v"(top2), [sent] "s"(0x7fffu));
+                (void)m0; (void)m2; (void)m3;
+                *sp_entry = (uint16_t)farc;
+                if (m5 == 0) break;
+                continue;
+            }
+#endif
             const bool h0 = c0min <= c0max;
             const bool h1 = c1min <= c1max;
             const bool swap = c1min < c0min;
