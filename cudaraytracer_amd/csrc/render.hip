@@ -1271,6 +1271,9 @@ typedef __attribute__((address_space(3))) uint16_t LdsU16;
 #ifndef RT_DIAG_NONE
 #define RT_DIAG_NONE 0
 #endif
+#ifndef RT_DIAG_OCT
+#define RT_DIAG_OCT 0
+#endif
 #ifndef RT_SLAB_ASM
 #define RT_SLAB_ASM 1
 #endif
@@ -1436,7 +1439,19 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 cnt.wnode += wave_leader();
                 if (__ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0) cnt.wnode_uniform += wave_leader();
                 const uint32_t act = (uint32_t)__popcll(__ballot(1));
-#if RT_DIAG_NONE
+#if RT_DIAG_OCT
+                // diagnostic build: counter 13 = node iterations whose tracing lanes share one direction octant,
+                // 14 = ... and one node (the scalar path)
+                {
+                    const uint32_t oct = (rd.x < 0.0f ? 1u : 0u) | (rd.y < 0.0f ? 2u : 0u) | (rd.z < 0.0f ? 4u : 0u);
+                    const bool oct_uniform = __ballot(oct != (uint32_t)__builtin_amdgcn_readfirstlane(oct)) == 0;
+                    const bool node_uniform = __ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0;
+                    if (wave_leader()) {
+                        cnt.idle_nt += oct_uniform ? 1u : 0u;
+                        cnt.idle_fin += (oct_uniform && node_uniform) ? 1u : 0u;
+                    }
+                }
+#elif RT_DIAG_NONE
                 // diagnostic build: counters 13/14 = visits whose two children both miss / ... that would be
                 // hit without the t_best clip (the visits a popped-entry distance test could skip)
                 {
