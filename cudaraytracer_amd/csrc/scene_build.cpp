@@ -336,6 +336,14 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
             *err = "hittable " + std::to_string(i) + ": non-finite centre or size";
             return RT_ERR_INVALID_SCENE;
         }
+        // A negative radius turns the reference's sphere box inside out (center - r > center + r,
+        // Hittable.cuh:114), which its AABB test (AABB.cuh:30-50) never enters while Sphere::Hit still would: whether
+        // the reference draws such a sphere depends on its tree shape.  The reference's editor keeps radii in
+        // [0, FLT_MAX] (CudaLayer.cpp:496), so the library rejects the case instead of guessing.
+        if (sphere && h.radius < 0.0f) {
+            *err = "hittable " + std::to_string(i) + ": negative sphere radius";
+            return RT_ERR_INVALID_SCENE;
+        }
         BuildPrim p;
         p.box = prim_box(h);
         for (int a = 0; a < 3; a++) p.centroid[a] = 0.5f * (p.box.lo[a] + p.box.hi[a]);

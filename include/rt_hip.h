@@ -83,7 +83,7 @@ typedef struct rt_hittable_desc {
     int32_t type;      /* rt_hittable_type */
     int32_t is_active; /* Hittable::isActive — inactive entries are dropped (Hittable.cuh:311-312) */
     float center[3];   /* Sphere::center / *Rect::center */
-    float radius;      /* RT_SPHERE */
+    float radius;      /* RT_SPHERE; >= 0 (the reference editor's range, CudaLayer.cpp:496), else RT_ERR_INVALID_SCENE */
     float width;       /* rects: XY width along x, XZ width along x, YZ width along z (Hittable.cuh:255-258) */
     float height;      /* rects: XY height along y, XZ height along z, YZ height along y */
     int32_t material;  /* index into rt_scene_desc.materials */

@@ -165,6 +165,7 @@ def test_empty_and_single_primitive_scenes():
     (lambda s: setattr(s.materials[0].albedo, "type", 5), -2),
     (lambda s: s.hittables[1].center.__setitem__(2, float("nan")), -2),  # no box for NaN geometry
     (lambda s: setattr(s.hittables[0], "radius", float("inf")), -2),
+    (lambda s: setattr(s.hittables[0], "radius", -0.5), -2),  # inside-out reference box (Hittable.cuh:114)
 ])
 def test_invalid_scenes_are_rejected(mutate, code):
     s = scenes.builtin(scenes.SCENE_THREE_SPHERES)
