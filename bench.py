@@ -1,40 +1,49 @@
 """Headline benchmark: Mray/s of the per-pixel path-trace kernel (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4] [--variant -1] [--tiled-devices 0,0]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--variant -1] [--tiled-devices 0,0]
 
 A step is one frame of the hot path (Kernel.cu:102-158 → librt_hip.so rt_render) over the whole image;
 inputs (scene tables, RNG state) are resident in HBM before the timed region.  Rays are counted by the
 kernel itself (one closest-hit query = one iteration of color()'s loop, Kernel.cu:39).
 
   --config c2 (default, the BASELINE metric): N = 1 renders config 2 (1920×1080, 64 spp, depth 8, RTIOW
-      final scene).  N > 1 (one process per GPU, launched by torch.distributed.run) is weak scaling: the
-      image grows to round(1920·√N) × round(1080·√N) (same camera and field of view, ≈2.07 M pixels per GPU),
-      split in block-cyclic 16-row bands, and every step ends with the RCCL gather to rank 0.
+      final scene).  N > 1 (one process per GPU) is weak scaling: the image grows to round(1920·√N) ×
+      round(1080·√N) (same camera and field of view, ≈2.07 M pixels per GPU), split in block-cyclic 16-row
+      bands, and every step ends with the RCCL gather to rank 0.
+  --config c3: BASELINE config 3 (3840×2160, 256 spp, depth 16, Cornell box), one GPU.
   --config c4: BASELINE config 4 as configured, strong scaling: one 7680×4320, 128 spp, depth 8 RTIOW frame
       split over the N ranks in 16-row bands (N = 1 renders all of it) + the RCCL gather, whose time is
       reported apart (gather_ms).
+  --config c5: BASELINE config 5 (1920×1080, 1 spp, depth 4, three 8192×4096 image textures), one GPU: a step
+      is one progressive frame of the scripted moving camera (new InputStruct, accumulation reset because the
+      camera moved, one RT_FLAG_ACCUMULATE frame).  Roofline against HBM.
   --tiled-devices d0,d1,…: single process, rt_tiled_* C ABI (one band rank per listed device, peer-copy
       gather): the path a C++ viewer uses without torch.distributed.
+
+Multi-GPU launch: under torch.distributed.run (WORLD_SIZE set) every process is one rank on device LOCAL_RANK.
+Without a launcher, `--gpus N` (N > 1) starts its own N ranks as a child `torch.distributed.run` before it
+touches any GPU, and fails if fewer than N devices are visible (`--share-gpu` rehearses N ranks on device 0).
+`--dry-run` exercises that launch path on the CPU: N gloo ranks gather synthetic bands, no GPU and no kernel.
 """
 from __future__ import annotations
 
 import argparse
-import re
 import json
 import math
 import os
+import re
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch initialises no GPU)
 import torch.distributed as dist  # noqa: E402
 
-from cudaraytracer_amd import abi, parallel, scenes  # noqa: E402
-from cudaraytracer_amd._lib import lib  # noqa: E402
-from cudaraytracer_amd.renderer import DeviceScene, Renderer  # noqa: E402
+from cudaraytracer_amd import parallel  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ≈ 8 TB/s per GPU
@@ -42,9 +51,98 @@ PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ≈ 8 TB/s per GPU
 # camera ray 40 per primary sample.
 FLOP_BOX, FLOP_PRIM, FLOP_RAY, FLOP_PRIMARY = 21, 23, 60, 40
 F_REF_PER_RAY = 21 * 50.7 + 23 * 6.9 + 60  # reference BVH on C2: ≈1.28 kFLOP/ray
+C5_FRAMES = 60  # C5's scripted orbit (scenes.moving_camera)
+
+METRICS = {
+    "c2": "Mray/s (and ms/frame) at 1920x1080, 64 spp, depth 8, random-spheres",
+    "c3": "Mray/s (and ms/frame) at 3840x2160, 256 spp, depth 16, Cornell-box emissive",
+    "c4": "Mray/s (and ms/frame) at 7680x4320, 128 spp, depth 8, random-spheres (8-GPU tile-split config)",
+    "c5": "Mray/s (and ms/frame) at 1920x1080, 1 spp progressive, depth 4, textured spheres + moving camera",
+}
+DATA = {
+    "c2": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
+    "c3": "synthetic: Cornell box of 6 rects (5 Lambertian walls + a DiffuseLight), black background",
+    "c4": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
+    "c5": "synthetic: 3 image-textured spheres + ground, three procedural 8192x4096 RGB8 textures "
+          "(the reference's asset size; its JPEGs are not decoded here), scripted orbit camera",
+}
 
 
-def cpu_baseline(cfg: scenes.Config, target_s: float) -> dict:
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5"))
+    ap.add_argument("--variant", type=int, default=-1, help="kernel variant (rt_set_variant); -1 = automatic")
+    ap.add_argument("--rng", choices=("xorwow", "philox"), default="xorwow",
+                    help="xorwow: the reference's per-pixel cuRAND state (parity mode, headline); philox: stateless "
+                         "Philox4x32-10 streams (RT_FLAG_RNG_PHILOX)")
+    ap.add_argument("--state-layout", choices=("soa", "curand"), default="soa",
+                    help="XORWOW states: soa = native six uint32 planes (RT_FLAG_STATE_SOA, 24 B/pixel, the same "
+                         "streams); curand = the reference's 48-B curandState structs (the LaunchKernel layout)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-philox-line", action="store_true", help="skip the secondary Philox-mode timing (N=1)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank renders on device 0 (use with --backend gloo)")
+    ap.add_argument("--tiled-devices", default="",
+                    help="single-process multi-device split through the rt_tiled C ABI, e.g. 0,1,2,3 (or 0,0 on one GPU)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank launch: N gloo ranks gather synthetic bands (no GPU)")
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args) -> int:
+    """`--gpus N` without a launcher: start N ranks as a child torch.distributed.run and wait for it.  This
+    process touches no GPU (torch.cuda.device_count() does not initialise one on this image)."""
+    if not args.dry_run and not args.share_gpu:
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, {visible} visible "
+                  f"(use --share-gpu to rehearse {args.gpus} ranks on one device)", file=sys.stderr, flush=True)
+            return 2
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args) -> None:
+    """The launch path without a GPU: every rank joins a gloo group and gathers a synthetic band buffer of the
+    configured frame (its global row indices), and rank 0 checks the reassembled frame."""
+    from cudaraytracer_amd.renderer import band_rows_of
+    from cudaraytracer_amd import scenes
+
+    rank, world, _ = parallel.env_rank()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --dry-run: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if world > 1:
+        parallel.init_process_group("gloo")
+    cfg = scenes.CONFIGS[args.config]
+    w, h = 64, cfg.height
+    rows = band_rows_of(h, parallel.DEFAULT_BAND_ROWS, world, rank)
+    local = torch.tensor(rows, dtype=torch.int64).repeat_interleave(w)
+    full = parallel.gather_bands(local, w, h, parallel.DEFAULT_BAND_ROWS) if world > 1 else local.view(h, w)
+    if rank == 0:
+        ok = bool(torch.equal(full, torch.arange(h, dtype=torch.int64)[:, None].expand(h, w)))
+        print(json.dumps({"dry_run": True, "world_size": world, "gpus": args.gpus, "config": args.config,
+                          "band_rows": parallel.DEFAULT_BAND_ROWS, "frame_ok": ok}), flush=True)
+        if not ok:
+            raise SystemExit("bench.py --dry-run: gathered frame differs")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, scene_desc, inputs, target_s: float) -> dict:
     """The CPU restatement of the path (oracle/rt_oracle.c built -O3 -march=native -ffp-contract=off on this
     host, OpenMP over rows; it computes the checker's bits, tests/test_oracle.py) on bounded row-strided samples
     of the same frame: on the job's whole CPU share, and on one core."""
@@ -60,8 +158,7 @@ def cpu_baseline(cfg: scenes.Config, target_s: float) -> dict:
     except OSError:
         pass
     L = po.native_lib(os.path.join(tempfile.gettempdir(), f"rt_oracle_native_{os.getuid()}"))
-    sc = po.OracleScene(scenes.builtin(cfg.scene), library=L)
-    inputs = cfg.inputs()
+    sc = po.OracleScene(scene_desc, library=L)
     st = po.init_states(cfg.width, cfg.height)
 
     def run(first: int, step: int, nthreads: int):
@@ -91,10 +188,11 @@ def cpu_baseline(cfg: scenes.Config, target_s: float) -> dict:
                       f"{dt1:.2f} s"}
 
 
-def secondary_mode(cfg: scenes.Config, scene: DeviceScene, inputs, steps: int, rng: str = "philox",
-                   state_layout: str = "curand") -> dict:
+def secondary_mode(cfg, scene, inputs, steps: int, rng: str = "philox", state_layout: str = "curand") -> dict:
     """Secondary figure: the same frames with the stateless Philox RNG (RT_FLAG_RNG_PHILOX, no per-pixel
     RNG state in HBM), or with the other XORWOW state layout."""
+    from cudaraytracer_amd.renderer import Renderer
+
     r = Renderer(cfg.width, cfg.height, rng=rng, state_layout=state_layout)
     r.render_init()
     r.render(scene, cfg.spp, cfg.depth, inputs)  # warm-up
@@ -128,8 +226,10 @@ def pmc_profile(config: str, rng: str, state_layout: str = "curand") -> dict:
     return {k: d[k] for k in keys if k in d}
 
 
-def run_tiled(args, cfg: scenes.Config) -> None:
+def run_tiled(args, cfg) -> None:
     """--tiled-devices: one process, rt_tiled_* (band rank r on devices[r], peer-copy gather into one frame)."""
+    from cudaraytracer_amd import scenes
+    from cudaraytracer_amd._lib import lib
     from cudaraytracer_amd.renderer import TiledRenderer
 
     devices = [int(d) for d in args.tiled_devices.split(",")]
@@ -160,67 +260,78 @@ def run_tiled(args, cfg: scenes.Config) -> None:
     t.close()
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=("c2", "c4"))
-    ap.add_argument("--variant", type=int, default=-1, help="kernel variant (rt_set_variant); -1 = automatic")
-    ap.add_argument("--rng", choices=("xorwow", "philox"), default="xorwow",
-                    help="xorwow: the reference's per-pixel cuRAND state (parity mode, headline); philox: stateless "
-                         "Philox4x32-10 streams (RT_FLAG_RNG_PHILOX)")
-    ap.add_argument("--state-layout", choices=("soa", "curand"), default="soa",
-                    help="XORWOW states: soa = native six uint32 planes (RT_FLAG_STATE_SOA, 24 B/pixel, the same "
-                         "streams); curand = the reference's 48-B curandState structs (the LaunchKernel layout)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-philox-line", action="store_true", help="skip the secondary Philox-mode timing (N=1)")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
-    ap.add_argument("--share-gpu", action="store_true",
-                    help="rehearsal on a 1-GPU box: every rank renders on device 0 (use with --backend gloo)")
-    ap.add_argument("--tiled-devices", default="",
-                    help="single-process multi-device split through the rt_tiled C ABI, e.g. 0,1,2,3 (or 0,0 on one GPU)")
-    args = ap.parse_args()
+def distinct_devices(world: int, device: int) -> int:
+    """Number of distinct physical GPUs the ranks render on (by device UUID; ranks may share one with --share-gpu)."""
+    try:
+        ident = str(torch.cuda.get_device_properties(device).uuid)
+    except Exception:  # noqa: BLE001 - older builds: fall back to the ordinal
+        ident = f"{socket.gethostname()}:{device}"
+    if world == 1:
+        return 1
+    ids = [None] * world
+    dist.all_gather_object(ids, ident)
+    return len(set(ids))
 
-    if args.tiled_devices:
-        run_tiled(args, scenes.CONFIGS[args.config])
-        return
+
+def run_rank(args) -> None:
+    from cudaraytracer_amd import abi, scenes
+    from cudaraytracer_amd._lib import lib
+    from cudaraytracer_amd.renderer import DeviceScene, Renderer
 
     rank, world, local_rank = parallel.env_rank()
     if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
+    if world > 1 and args.config in ("c3", "c5"):
+        raise SystemExit(f"bench.py: --config {args.config} is a one-GPU configuration (BASELINE.json configs 3, 5)")
     device = 0 if args.share_gpu else local_rank
     if world > 1:
+        visible = torch.cuda.device_count()
+        if device >= visible:
+            raise SystemExit(f"bench.py: rank {rank} wants GPU {device}, {visible} visible")
         torch.cuda.set_device(device)
         parallel.init_process_group(args.backend)
     red_dev = torch.device("cpu") if args.backend == "gloo" else torch.device("cuda", device)
     cfg = scenes.CONFIGS[args.config]
     strong = args.config == "c4"  # one fixed frame split over the ranks
-    if world > 1 and not strong:
+    progressive = args.config == "c5"
+    if world > 1 and args.config == "c2":
         s = math.sqrt(world)
         cfg = cfg.scaled(int(round(cfg.width * s)), int(round(cfg.height * s)))
     lib().rt_set_variant(args.variant)
+    n_gpus = distinct_devices(world, device)
 
     band = parallel.DEFAULT_BAND_ROWS if world > 1 else cfg.height
     r = Renderer(cfg.width, cfg.height, device=device, band_rows=band, num_ranks=world, rank=rank, rng=args.rng,
                  state_layout=args.state_layout)
-    scene = DeviceScene(scenes.builtin(cfg.scene))
+    scene_desc = cfg.scene_desc()
+    scene = DeviceScene(scene_desc)
     inputs = cfg.inputs()
     r.render_init()
+    frame_flags = abi.RT_FLAG_ACCUMULATE if progressive else 0
 
     # Counting pass (untimed, RNG state not advanced): executed box / primitive tests for F_exec.
     r.counters.zero_()
-    r.render(scene, cfg.spp, cfg.depth, inputs, flags=abi.RT_FLAG_COUNT_TESTS | abi.RT_FLAG_NO_STATE_WRITEBACK)
+    r.render(scene, cfg.spp, cfg.depth, inputs,
+             flags=frame_flags | abi.RT_FLAG_COUNT_TESTS | abi.RT_FLAG_NO_STATE_WRITEBACK)
     torch.cuda.synchronize()
     c = [int(x) for x in r.counters.tolist()]
     f_launch = FLOP_BOX * c[1] + FLOP_PRIM * c[2] + FLOP_RAY * c[0] + FLOP_PRIMARY * c[3]
 
+    frame_no = [0]
+
+    def frame_inputs():
+        """C5: the next pose of the scripted orbit (the camera moves every frame, so the accumulation restarts)."""
+        if not progressive:
+            return inputs
+        pos, fwd = scenes.moving_camera(frame_no[0] % C5_FRAMES, C5_FRAMES)
+        frame_no[0] += 1
+        r.reset_accumulation()
+        return scenes.camera_inputs(pos, fwd, cfg.fov)
+
     def step():
-        r.render(scene, cfg.spp, cfg.depth, inputs)
+        r.render(scene, cfg.spp, cfg.depth, frame_inputs(), flags=frame_flags)
         if world > 1:
-            parallel.gather_bands(r.pos, cfg.width, cfg.height, band)
+            parallel.gather_bands(r.pos, cfg.width, cfg.height, band, reuse=True)
 
     for _ in range(args.warmup):
         step()
@@ -236,10 +347,10 @@ def main() -> None:
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        r.render(scene, cfg.spp, cfg.depth, inputs)
+        r.render(scene, cfg.spp, cfg.depth, frame_inputs(), flags=frame_flags)
         ev[i][1].record(stream)
         if world > 1:
-            parallel.gather_bands(r.pos, cfg.width, cfg.height, band)
+            parallel.gather_bands(r.pos, cfg.width, cfg.height, band, reuse=True)
         ev[i][2].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -257,27 +368,12 @@ def main() -> None:
     rays_all = int(tot[0])
 
     if rank == 0:
-        achieved = f_launch / (kernel_ms * 1e-3) / 1e12
-        # HBM bytes per launch: the committed N=1 C2 PMC summary.  A rank's bytes do not depend on spp (per pixel:
-        # RNG state in and out, one RGBA8 store), so other frame shapes scale it by the rank's pixel count.
-        pmc = pmc_profile("c2", args.rng, args.state_layout)
-        c2 = scenes.CONFIGS["c2"]
-        pix_scale = r.local_rows * cfg.width / (c2.width * c2.height)
-        if "hbm_bytes_per_launch" in pmc and pix_scale != 1.0:
-            for k in ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch"):
-                if k in pmc:
-                    pmc[k] = round(pmc[k] * pix_scale)
-            pmc["scaled"] = True
-        rays_per_launch = c[0]
-        hbm_gbps = (round(pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 2)
-                    if "hbm_bytes_per_launch" in pmc else None)
-        metric = ("Mray/s (and ms/frame) at 1920x1080, 64 spp, depth 8, random-spheres" if not strong else
-                  "Mray/s (and ms/frame) at 7680x4320, 128 spp, depth 8, random-spheres (8-GPU tile-split config)")
         line = {
-            "metric": metric,
+            "metric": METRICS[args.config],
             "value": round(rays_all / elapsed / 1e6, 2),
             "unit": "Mray/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
+            "world_size": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -287,55 +383,121 @@ def main() -> None:
             "dtype": "f32",
             "rng": args.rng,
             "state_layout": args.state_layout if args.rng == "xorwow" else None,
-            "data": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
+            "data": DATA[args.config],
             "config": {
                 "workload": (f"{args.config}: {cfg.width}x{cfg.height}, {cfg.spp} spp, depth {cfg.depth}, "
                              + ", ".join(part for part in scenes.CONFIGS[args.config].description.split(", ")
                                          if not re.match(r"\d+ GPUs$|\d+x\d+$|\d+ spp|depth \d+$", part))),
                 "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
-                "parallelism": (f"{world} rank(s) x 16-row bands + {'RCCL' if args.backend == 'nccl' else args.backend} gather"
-                                if world > 1 else "1 GPU"),
+                "parallelism": (f"{world} rank(s) on {n_gpus} GPU(s) x 16-row bands + "
+                                f"{'RCCL' if args.backend == 'nccl' else args.backend} gather" if world > 1 else "1 GPU"),
                 "kernel_variant": args.variant,
             },
             "kernel_ms": round(kernel_ms, 3),
             "gather_ms": round(gather_ms, 3) if world > 1 else 0.0,
             "rays_per_frame": rays_all // args.steps,
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved, 3),
-                "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                "traffic": pmc.get("hbm_bytes_per_launch"),
-                "traffic_source": (("rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_c2_n1.json"
-                                    + (" (per-pixel bytes x this rank's pixels)" if pmc.get("scaled") else ""))
-                                   if "hbm_bytes_per_launch" in pmc else None),
-                "algorithmic_hbm_bytes": pmc.get("algorithmic_bytes_per_launch"),
-                "hbm_GBps_achieved": hbm_gbps,
-                "hbm_frac_of_peak": round(hbm_gbps / PEAK_HBM_GBPS, 5) if hbm_gbps is not None else None,
-                "hbm_per_rank": world > 1,
-                "simd_lane_utilization": pmc.get("valu_lane_utilization"),
-                "waves_per_simd": pmc.get("avg_waves_per_simd"),
-                "ta_busy_frac": pmc.get("ta_busy_frac_per_cu"),
-                "flop_per_launch": f_launch,
-                "flop_per_ray_exec": round(f_launch / max(1, c[0]), 1),
-                "flop_per_ray_ref_bvh": round(F_REF_PER_RAY, 1),
-                "box_tests_per_ray": round(c[1] / max(1, c[0]), 2),
-                "prim_tests_per_ray": round(c[2] / max(1, c[0]), 2),
-                "rays_per_launch_rank0": rays_per_launch,
-            },
         }
-        if world == 1 and args.rng == "xorwow" and not args.no_philox_line and not strong:
+        if progressive:
+            line["roofline"] = hbm_roofline(args, cfg, r, c, kernel_ms)
+        else:
+            line["roofline"] = valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world)
+        if world == 1 and args.rng == "xorwow" and not args.no_philox_line and args.config in ("c2", "c3"):
             line["philox_mode"] = secondary_mode(cfg, scene, inputs, args.steps)
-            other = "curand" if args.state_layout == "soa" else "soa"
-            line[f"{other}_state_layout"] = dict(secondary_mode(cfg, scene, inputs, args.steps, "xorwow", other),
-                                                 hbm_bytes_per_launch=pmc_profile(args.config, "xorwow", other).get(
-                                                     "hbm_bytes_per_launch"))
+            if args.config == "c2":
+                other = "curand" if args.state_layout == "soa" else "soa"
+                line[f"{other}_state_layout"] = dict(secondary_mode(cfg, scene, inputs, args.steps, "xorwow", other),
+                                                     hbm_bytes_per_launch=pmc_profile(args.config, "xorwow", other).get(
+                                                         "hbm_bytes_per_launch"))
         if world == 1 and not args.no_cpu_baseline and not strong:
-            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+            cpu_inputs = inputs if not progressive else scenes.camera_inputs(*scenes.moving_camera(0, C5_FRAMES), cfg.fov)
+            line["cpu_baseline"] = cpu_baseline(cfg, scene_desc, cpu_inputs, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world) -> dict:
+    """VALU-bound roofline: counted algorithmic FLOP of rank 0's launch ÷ the kernel
+    time (max over ranks), against the FP32 vector peak; HBM bytes from the committed PMC summary."""
+    from cudaraytracer_amd import scenes
+
+    achieved = f_launch / (kernel_ms * 1e-3) / 1e12
+    # HBM bytes per launch: the committed N=1 PMC summary of this config.  A rank's bytes do not depend on spp
+    # (per pixel: RNG state in and out, one RGBA8 store), so other frame shapes scale it by the rank's pixels.
+    pmc = pmc_profile(args.config if args.config != "c4" else "c2", args.rng, args.state_layout)
+    base = scenes.CONFIGS[args.config if args.config != "c4" else "c2"]
+    pix_scale = r.local_rows * cfg.width / (base.width * base.height)
+    if "hbm_bytes_per_launch" in pmc and pix_scale != 1.0:
+        for k in ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch"):
+            if k in pmc:
+                pmc[k] = round(pmc[k] * pix_scale)
+        pmc["scaled"] = True
+    hbm_gbps = round(pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9, 2) if "hbm_bytes_per_launch" in pmc else None
+    return {
+        "bound": "valu",
+        "achieved": round(achieved, 3),
+        "peak": PEAK_FP32_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+        "scope": ("per rank: rank 0's counted FLOP per launch / the slowest rank's kernel time, against one GPU's "
+                  "peak" if world > 1 else "one launch = one frame"),
+        "traffic": pmc.get("hbm_bytes_per_launch"),
+        "traffic_source": ((f"rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_{args.config if args.config != 'c4' else 'c2'}_n1.json"
+                            + (" (per-pixel bytes x this rank's pixels)" if pmc.get("scaled") else ""))
+                           if "hbm_bytes_per_launch" in pmc else None),
+        "algorithmic_hbm_bytes": pmc.get("algorithmic_bytes_per_launch"),
+        "hbm_GBps_achieved": hbm_gbps,
+        "hbm_frac_of_peak": round(hbm_gbps / PEAK_HBM_GBPS, 5) if hbm_gbps is not None else None,
+        "hbm_per_rank": world > 1,
+        "simd_lane_utilization": pmc.get("valu_lane_utilization"),
+        "waves_per_simd": pmc.get("avg_waves_per_simd"),
+        "ta_busy_frac": pmc.get("ta_busy_frac_per_cu"),
+        "flop_per_launch": f_launch,
+        "flop_per_ray_exec": round(f_launch / max(1, c[0]), 1),
+        "flop_per_ray_ref_bvh": round(F_REF_PER_RAY, 1),
+        "box_tests_per_ray": round(c[1] / max(1, c[0]), 2),
+        "prim_tests_per_ray": round(c[2] / max(1, c[0]), 2),
+        "rays_per_launch_rank0": c[0],
+    }
+
+
+def hbm_roofline(args, cfg, r, c, kernel_ms) -> dict:
+    """C5 is the one configuration whose frame moves HBM bytes worth a roofline: per pixel
+    the RNG state in and out (24 + 24 B used, either layout; none for Philox), the float4 accumulator read and
+    written (32 B) and the RGBA8 store (4 B).  The texel gathers (3 B per image-texture lookup, at most one per
+    ray) are not in the algorithmic figure; the PMC traffic includes them."""
+    px = cfg.width * r.local_rows
+    per_px = (0 if args.rng == "philox" else 48) + 32 + 4
+    algo = per_px * px
+    achieved = algo / (kernel_ms * 1e-3) / 1e9
+    pmc = pmc_profile("c5", args.rng, args.state_layout)
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 2),
+        "peak": PEAK_HBM_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / PEAK_HBM_GBPS, 4),
+        "traffic": pmc.get("hbm_bytes_per_launch"),
+        "traffic_source": "rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_c5_n1.json" if pmc else None,
+        "algorithmic_hbm_bytes": algo,
+        "algorithmic_bytes_per_pixel": per_px,
+        "rays_per_launch": c[0],
+    }
+
+
+def main() -> None:
+    args = parse_args()
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1 and not args.tiled_devices:
+        sys.exit(self_launch(args))
+    if args.dry_run:
+        dry_run(args)
+        return
+    if args.tiled_devices:
+        from cudaraytracer_amd import scenes
+        run_tiled(args, scenes.CONFIGS[args.config])
+        return
+    run_rank(args)
 
 
 if __name__ == "__main__":

@@ -252,6 +252,7 @@ struct LaunchEntry {
     std::vector<rt_hittable_desc> hittables;
     std::vector<rt_material_desc> materials;
     std::vector<ImageKey> images;
+    int texel_bytes = 0;  // device bytes per texel of the uploaded block (RT_TUNE_TEXEL_LAYOUT when it was made)
     // shared with the LaunchKernel calls rendering it: an entry evicted or rebuilt by another thread frees
     // its device scene only when the last of them has finished
     std::shared_ptr<rt_scene> scene;
@@ -310,7 +311,10 @@ int reference_scene_for_launch(const void* world, std::shared_ptr<rt_scene>* out
         ent->last_use = ++g_launch_clock;
         const bool geometry = !ent->scene || !same_bytes(ent->hittables, f.hittables) ||
                               ent->materials.size() != f.materials.size();
-        const bool new_images = !ent->scene || !(ent->images == images);
+        // the image table of a rebuilt scene takes this thread's texel layout: a block uploaded in the other
+        // layout cannot be shared with it (its offsets and strides differ), so a layout change re-uploads
+        const int texel_bytes = g_texel_bytes == 4 ? 4 : 3;
+        const bool new_images = !ent->scene || !(ent->images == images) || ent->texel_bytes != texel_bytes;
         if (geometry || new_images) {
             rt_scene_desc d = f.desc();
             HostScene h;
@@ -320,6 +324,7 @@ int reference_scene_for_launch(const void* world, std::shared_ptr<rt_scene>* out
             r = create_device_scene(h, &fresh, new_images ? nullptr : ent->scene->texel_block);
             if (r) return r;
             ent->scene = own_scene(fresh, device);
+            ent->texel_bytes = texel_bytes;
         } else if (!same_bytes(ent->materials, f.materials)) {
             r = rt_scene_update_materials(ent->scene.get(), f.materials.data(), (uint32_t)f.materials.size());
             if (r) return r;

@@ -2106,7 +2106,9 @@ struct AutoChoice {
 constexpr uint32_t kAutoSpp = 64;  // from here on v3 always (configs 2-4: 64-256 spp)
 std::mutex g_auto_mu;
 // never destroyed (holds HIP events, see g_plans)
-std::map<AutoKey, std::unique_ptr<AutoChoice>>& g_auto = *new std::map<AutoKey, std::unique_ptr<AutoChoice>>();
+// entries held by shared_ptr: a frame being timed keeps its AutoChoice (and events) alive even if another
+// thread clears the map meanwhile
+std::map<AutoKey, std::shared_ptr<AutoChoice>>& g_auto = *new std::map<AutoKey, std::shared_ptr<AutoChoice>>();
 
 // never destroyed: plans free device memory, which must not run after the HIP runtime has shut down
 std::map<PlanKey, std::shared_ptr<TilePlan>>& g_plans = *new std::map<PlanKey, std::shared_ptr<TilePlan>>();
@@ -2137,8 +2139,9 @@ thread_local int g_persistent_waves = 0;  // 0: occupancy query
 constexpr size_t kLdsLimit = 160 * 1024;
 
 // Work-queue heads of the persistent kernel: a ring of counters per device, one slot per launch, zeroed
-// on the launch's stream right before it.  Slots are 64 B apart; a slot is reused only after
-// kQueueSlots further launches on that device, far more than can be in flight at once.
+// on the launch's stream right before it.  A slot is kQueueBytes (the kQueueCounters heads 128 B apart plus
+// the exhausted-heads word) and is reused after kQueueSlots further persistent launches on that device: a
+// caller may keep at most kQueueSlots persistent launches in flight per device (rt_hip.h, rt_render).
 constexpr uint32_t kQueueSlots = 256;
 constexpr uint32_t kQueueBytes = (dev::kQueueCounters + 1u) * 128u;  // one launch's heads + exhausted-heads word
 constexpr int kMaxDevices = 64;
@@ -2284,6 +2287,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (a->tiling.local_rows == 0 || a->width == 0 || a->height == 0) return RT_OK;  // nothing to render
     const bool philox = (a->flags & RT_FLAG_RNG_PHILOX) != 0;
     if (!a->state && !philox) { set_error("rt_render: state is NULL"); return RT_ERR_INVALID_ARGUMENT; }
+    if (a->reserved != 0 || a->reserved2 != 0) { set_error("rt_render: reserved fields must be 0"); return RT_ERR_INVALID_ARGUMENT; }
     if (!a->pos && !a->radiance && !a->accum) { set_error("rt_render: no output buffer"); return RT_ERR_INVALID_ARGUMENT; }
     if ((a->flags & RT_FLAG_ACCUMULATE) && !a->accum) { set_error("rt_render: ACCUMULATE without accum"); return RT_ERR_INVALID_ARGUMENT; }
     if (a->width == 0 || a->height == 0) return RT_OK;
@@ -2394,7 +2398,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // 2's wave in 5 KB of LDS, 8 waves per SIMD (config 2: 17.05 vs 17.8 ms with 15-word parking; config 3,
     // depth 16: 365 vs 408 ms for v4).  Compact parking falls back to 15 words where its packed counters
     // would overflow.
-    AutoChoice* trial = nullptr;  // this frame is timed for the automatic choice: events ev[trial_slot..+1]
+    std::shared_ptr<AutoChoice> trial;  // this frame is timed for the automatic choice: events ev[trial_slot..+1]
     int trial_slot = 0;
     const bool automatic = variant < 0 || variant >= kNumVariants;
     if (automatic) {
@@ -2408,9 +2412,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
             auto it = g_auto.find(key);
             if (it == g_auto.end()) {
                 if (g_auto.size() >= 64) g_auto.clear();
-                it = g_auto.emplace(key, std::make_unique<AutoChoice>()).first;
+                it = g_auto.emplace(key, std::make_shared<AutoChoice>()).first;
             }
-            AutoChoice& ac = *it->second;
+            const std::shared_ptr<AutoChoice> held = it->second;
+            AutoChoice& ac = *held;
             if (ac.chosen >= 0) {
                 variant = ac.chosen;
             } else if (ac.stage < 3) {
@@ -2419,7 +2424,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                     trial_slot = ac.stage == 1 ? 0 : 2;
                     if ((ac.ev[trial_slot] || hipEventCreate(&ac.ev[trial_slot]) == hipSuccess) &&
                         (ac.ev[trial_slot + 1] || hipEventCreate(&ac.ev[trial_slot + 1]) == hipSuccess))
-                        trial = &ac;
+                        trial = held;
                 }
                 ac.stage++;
             } else if (ac.ev[1] && ac.ev[3] && hipEventQuery(ac.ev[1]) == hipSuccess &&
@@ -2519,13 +2524,13 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     (void)hipGetLastError();
     hipLaunchKernelGGL(fn, dim3(grid), dim3(V.block), lds_bytes, s, P);
     int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
+    if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);  // the render kernel alone (v4 has no plan step)
     if (rc == RT_OK && plan) {  // the next launch on this stream dispatches this frame's costliest tiles first
         hipLaunchKernelGGL(dev::plan_order_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)plan->cost, plan->order,
                            tiles);
         rc = hip_check(hipGetLastError(), "rt_render: plan kernel launch", RT_ERR_LAUNCH);
         if (rc == RT_OK) plan->valid.store(true);
     }
-    if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);
     if (g_timing) {
         (void)hipEventRecord(e1, s);
         if (rc == RT_OK && hipEventSynchronize(e1) == hipSuccess) {

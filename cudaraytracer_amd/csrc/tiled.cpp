@@ -96,6 +96,10 @@ int rt_tiled_create(const rt_tiled_desc* desc, const rt_scene_desc* scene, rt_ti
         set_error("rt_tiled_create: empty image");
         return RT_ERR_INVALID_ARGUMENT;
     }
+    if ((desc->flags & ~(uint32_t)RT_FLAG_RNG_PHILOX) || desc->reserved != 0) {
+        set_error("rt_tiled_create: flags other than RT_FLAG_RNG_PHILOX, or reserved != 0");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
     int ndev = 0;
     if (int rc = hip_err(hipGetDeviceCount(&ndev), "hipGetDeviceCount")) return rc;
     for (uint32_t r = 0; r < desc->num_ranks; r++)
@@ -155,6 +159,20 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
         set_error("rt_tiled_render: NULL argument");
         return RT_ERR_INVALID_ARGUMENT;
     }
+    // Frame flags the band ranks can honour: each rank's state buffer is rt_curand_state structs seeded by
+    // rt_render_init (so RT_FLAG_STATE_SOA would read them as planes, past their end for short ranks), the
+    // RNG mode is fixed at creation and there is no per-rank accumulation buffer.
+    constexpr uint32_t kFrameFlags = RT_FLAG_FAITHFUL_GRID | RT_FLAG_NO_STATE_WRITEBACK | RT_FLAG_COUNT_TESTS |
+                                     RT_FLAG_RIUS_LEFT_TO_RIGHT;
+    if (f->flags & ~kFrameFlags) {
+        set_error("rt_tiled_render: frame flags outside FAITHFUL_GRID | NO_STATE_WRITEBACK | COUNT_TESTS | "
+                  "RIUS_LEFT_TO_RIGHT");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    if (f->reserved != 0 || (f->rng_frame_set != 0 && f->rng_frame_set != 1)) {
+        set_error("rt_tiled_render: reserved fields must be 0 and rng_frame_set 0 or 1");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     DeviceGuard guard;
     const uint32_t W = t->desc.width, H = t->desc.height, B = t->desc.band_rows, N = t->desc.num_ranks;
@@ -196,8 +214,7 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
             a.height = H;
             a.samples_per_pixel = f->samples_per_pixel;
             a.max_depth = f->max_depth;
-            a.flags = (f->flags & ~(uint32_t)(RT_FLAG_ACCUMULATE | RT_FLAG_RNG_PHILOX)) |
-                      (philox ? (uint32_t)RT_FLAG_RNG_PHILOX : 0u);
+            a.flags = f->flags | (philox ? (uint32_t)RT_FLAG_RNG_PHILOX : 0u);
             a.tiling = rt_tiling{B, N, r, k.local_rows};
             a.inputs = f->inputs;
             a.rng_seed = t->desc.seed;

@@ -74,21 +74,25 @@ def unshuffle_into(full: torch.Tensor, recv: list, height: int, width: int, band
 
 
 def gather_bands(local: torch.Tensor, width: int, height: int, band_rows: int, dst: int = 0,
-                 group=None) -> torch.Tensor | None:
-    """Gather every rank's (local_rows·W) framebuffer to `dst` and return the (H, W) image there (a buffer
-    reused by later calls of the same shape).  With the gloo backend (CPU tests, single-GPU rehearsals)
-    device buffers are staged through host memory."""
+                 group=None, reuse: bool = False) -> torch.Tensor | None:
+    """Gather every rank's (local_rows·W) framebuffer to `dst` and return the (H, W) image there.  The result
+    is a fresh tensor unless `reuse` is set: then it is a module-owned buffer that the next gather of the same
+    shape overwrites (the bench, which gathers every step and keeps no frame).  With the gloo backend (CPU
+    tests, single-GPU rehearsals) device buffers are staged through host memory."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     counts = local_row_counts(height, band_rows, world)
     max_rows = max(counts)
     via_host = local.is_cuda and dist.get_backend(group) == "gloo"
     dev = torch.device("cpu") if via_host else local.device
-    key = (id(group), world, rank, dst, max_rows, width, height, band_rows, local.dtype, str(dev))
+    # keyed by the group object itself (held in the key, so a destroyed group's id cannot be reused by another)
+    key = (group, world, rank, dst, max_rows, width, height, band_rows, local.dtype, str(dev))
     send, recv, full = _buffers(key, world, rank, dst, max_rows, width, height, local.dtype, dev)
     send[: local.numel()].copy_(local.reshape(-1))
     dist.gather(send, recv, dst=dst, group=group)
     if rank != dst:
         return None
     unshuffle_into(full, recv, height, width, band_rows)
-    return full.to(local.device) if via_host else full
+    if via_host:
+        return full.to(local.device)
+    return full if reuse else full.clone()

@@ -265,7 +265,9 @@ typedef struct rt_render_args {
     uint32_t reserved2;       /* must be 0 */
 } rt_render_args;
 
-/* One frame of the per-pixel render kernel (Kernel.cu:102-158) on `stream`. */
+/* One frame of the per-pixel render kernel (Kernel.cu:102-158) on `stream`, asynchronous.  At most 256
+ * frames may be in flight per device at once (the persistent kernel's work-queue slots are reused after
+ * 256 launches); synchronise at least that often when queueing frames on several streams. */
 int rt_render(const rt_scene* scene, const rt_render_args* args, rt_stream stream);
 
 /* Kernel duration of the last rt_render on this thread measured with HIP events on its stream

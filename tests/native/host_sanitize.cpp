@@ -231,6 +231,13 @@ static void outputs_and_misc() {
     CHECK(rc == RT_OK ? t != nullptr : t == nullptr);
     if (t) rt_tiled_destroy(t);
     CHECK(rt_tiled_create(nullptr, &d, &t) == RT_ERR_INVALID_ARGUMENT);
+    // creation flags: only the RNG mode; STATE_SOA would make the ranks read their struct states as planes
+    rt_tiled_desc bad = td;
+    bad.flags = RT_FLAG_STATE_SOA;
+    CHECK(rt_tiled_create(&bad, &d, &t) == RT_ERR_INVALID_ARGUMENT);
+    bad = td;
+    bad.reserved = 1;
+    CHECK(rt_tiled_create(&bad, &d, &t) == RT_ERR_INVALID_ARGUMENT);
     CHECK(rt_tiled_render(nullptr, nullptr, nullptr) == RT_ERR_INVALID_ARGUMENT);
     CHECK(rt_gl_register_texture(0, 0x0DE1, nullptr) == RT_ERR_INVALID_ARGUMENT);
 }

@@ -310,3 +310,57 @@ def test_tiled_c_abi_c4_frame_equals_single_rank_rows():
     r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), frame=4)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(tiled, r.image())
+
+
+def test_tiled_render_rejects_frame_flags_it_cannot_honour():
+    """rt_tiled ranks hold rt_curand_state structs, so an RT_FLAG_STATE_SOA (or ACCUMULATE) frame flag
+    must be refused, not passed to rt_render (which would read the structs as planes, past their end)."""
+    from cudaraytracer_amd._lib import RTError
+    from cudaraytracer_amd.renderer import TiledRenderer
+    cfg = scenes.CONFIGS["c2"].scaled(64, 17, 2)
+    t = TiledRenderer(cfg.width, cfg.height, [0, 0], scenes.builtin(cfg.scene))
+    try:
+        for bad in (abi.RT_FLAG_STATE_SOA, abi.RT_FLAG_ACCUMULATE, abi.RT_FLAG_RNG_PHILOX):
+            with pytest.raises(RTError, match="frame flags"):
+                t.render(cfg.spp, cfg.depth, cfg.inputs(), flags=bad)
+        t.render(cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)  # still usable
+    finally:
+        t.close()
+
+
+def test_launch_kernel_cache_follows_the_texel_layout():
+    """a geometry rebuild of a cached LaunchKernel scene after RT_TUNE_TEXEL_LAYOUT changed must not
+    pair the new image table with the texel block uploaded in the other layout."""
+    import ctypes as C
+
+    import refgraph
+    from cudaraytracer_amd._lib import lib
+
+    cfg = scenes.CONFIGS["c5"].scaled(96, 64, 2)
+    W, H = cfg.width, cfg.height
+    base = scenes.builtin(cfg.scene)  # three 1024x512 textures
+    sc = scenes.Scene(base.hittables, base.materials, list(base.images))
+    graph = refgraph.build_graph(sc)
+    world = C.c_void_p(C.addressof(graph.world))
+    dev = torch.device("cuda", 0)
+    pos = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    state = torch.zeros(W * H * abi.STATE_WORDS, dtype=torch.int32, device=dev)
+    lib().LaunchRenderInit(abi.Dim3(W // 16, H // 16, 1), abi.Dim3(16, 16, 1), W, H, C.c_void_p(state.data_ptr()))
+    st = po.init_states(W, H, full=False)
+    sph = [o for o in graph.keep if isinstance(o, refgraph.Sphere) and abs(o.radius - 1.5) < 1e-6][0]
+    idx = [i for i in range(sc.num_hittables)
+           if sc.hittables[i].type == abi.RT_SPHERE and abs(sc.hittables[i].radius - 1.5) < 1e-6][0]
+    prev = lib().rt_set_tuning(6, 3)
+    try:
+        for layout, y in ((3, None), (4, 1.25), (3, 1.1), (4, None)):
+            lib().rt_set_tuning(6, layout)
+            if y is not None:  # move the sphere: the cache rebuilds the BVH and keeps (or not) the texel block
+                sph.center.e[1] = y
+                sc.hittables[idx].center[1] = y
+            lib().LaunchKernel(C.c_void_p(pos.data_ptr()), W, H, cfg.spp, cfg.depth, world,
+                               C.c_void_p(state.data_ptr()), cfg.inputs())
+            img = pos.cpu().numpy().view(np.uint32).reshape(H, W)
+            ref, _, _ = po.render(po.OracleScene(sc), W, H, cfg.spp, cfg.depth, cfg.inputs(), st, faithful_grid=True)
+            np.testing.assert_array_equal(img, ref, err_msg=f"texel layout {layout}")
+    finally:
+        lib().rt_set_tuning(6, prev)

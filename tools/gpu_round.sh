@@ -2,12 +2,13 @@
 # One GPU session (run through gpurun from the repo root): parity tests, smoke, bench + rocprofv3 kernel
 # summary, per-config timings.  Every GPU step has its own time limit and the session stops at the first
 # GPU fault, abort, segfault or timeout (pytest rc 1 = test failures only, which does not stop it).
-#   STEPS="tests smoke bench prof configs rehearse"   (default: all but rehearse)   PYTEST_ARGS=...   BENCH_ARGS=...
+#   STEPS="tests smoke bench prof benchcfg configs rehearse"   (default: tests smoke bench prof benchcfg)
+#   PYTEST_ARGS=...   BENCH_ARGS=...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-STEPS=${STEPS:-tests smoke bench prof configs}
+STEPS=${STEPS:-tests smoke bench prof benchcfg}
 for step in $STEPS; do
   case $step in
     tests)
@@ -23,11 +24,20 @@ for step in $STEPS; do
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
         python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench_prof.log 2>&1 || exit $? ;;
-    rehearse)  # bench.py's N > 1 path with every rank on device 0 (gloo gather): weak (C2) and strong (C4) scaling
+    benchcfg)  # driver-shaped lines for BASELINE configs 3 and 5
+      for cfg in c5 c3; do
+        timeout -k 10 400 python bench.py --config $cfg --steps ${CFG_STEPS:-5} --warmup 2 ${BENCH_ARGS:-} \
+          > gpurun_out/bench_$cfg.log 2>&1 || exit $?
+        tail -1 gpurun_out/bench_$cfg.log
+      done ;;
+    selfcheck)  # bench.py --gpus 2 on a 1-GPU box must fail (no N=1 line)
+      if timeout -k 10 120 python bench.py --gpus 2 --steps 1 --warmup 0 > gpurun_out/selfcheck.log 2>&1; then
+        echo "selfcheck: --gpus 2 ran on one GPU" ; exit 3; fi
+      tail -2 gpurun_out/selfcheck.log ;;
+    rehearse)  # bench.py's self-launched N > 1 path with every rank on device 0 (gloo gather): C2 weak, C4 strong
       for n in ${REHEARSE_N:-2 4}; do
         for cfg in c2 c4; do
-          timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-            --master-port $((29400 + n)) bench.py --gpus $n --steps 3 --warmup 1 --config $cfg --backend gloo \
+          timeout -k 10 400 python bench.py --gpus $n --steps 3 --warmup 1 --config $cfg --backend gloo \
             --share-gpu --no-cpu-baseline --no-philox-line > gpurun_out/rehearse_${cfg}_n$n.log 2>&1 || exit $?
           tail -1 gpurun_out/rehearse_${cfg}_n$n.log
         done
