@@ -133,21 +133,13 @@ __device__ __forceinline__ float uniform(Rng& s) {
     s.v1 = s.v2;
     s.v2 = s.v3;
     s.v3 = s.v4;
-#ifdef RT_XORWOW_SHL
-    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
-#else
     uint32_t t2;  // t << 1 as a full-rate add (v_lshlrev_b32 issues at half rate on gfx950)
     asm("v_add_u32 %0, %1, %1" : "=v"(t2) : "v"(t));
     s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ t2);
-#endif
     s.d += 362437u;
     uint32_t x = s.v4 + s.d;
     // x·2^-32 + 2^-33 (_curand_uniform): the product is exact, so one fma rounds like the mul + add
-#ifdef RT_NO_FMA_UNIFORM
-    return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
-#else
     return __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f / 2.0f);
-#endif
 }
 
 // RandomInUnitSphere (Math.cuh:252-260) with Random() (Math.cuh:231-234).  rtl: the components of
@@ -166,23 +158,9 @@ template <class R> __device__ __forceinline__ void draw3(R& s, float& a, float& 
 }
 
 // 2·ξ − 1 of each component with one fma: 2·ξ is exact, so it rounds like the reference's mul + sub.  The
-// fill order is a launch-uniform branch around the loop, not a select per attempt.
-template <bool RTL, class R>
-__device__ __forceinline__ f3 random_in_unit_sphere_order(R& s) {
-    f3 p;
-    do {
-        float a, b, c;
-        draw3(s, a, b, c);
-        const f3 r = RTL ? mk(c, b, a) : mk(a, b, c);
-        p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
-    } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
-    return p;
-}
+// fill order is two selects per attempt (a launch-uniform branch around the loop measured the same).
 template <class R>
 __device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
-#ifdef RT_RIUS_BRANCH
-    return rtl ? random_in_unit_sphere_order<true>(s) : random_in_unit_sphere_order<false>(s);
-#else
     f3 p;
     do {
         float a, b, c;
@@ -191,7 +169,6 @@ __device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
         p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
     } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
     return p;
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -242,10 +219,7 @@ constexpr int kBlock = 256;
 // v4 work queue: the frame's work indices are split into this many contiguous ranges, each with its own
 // head 128 B from the next — one shared head serialises every wave's atomic in one L2 channel (≈ 16 ns
 // each: 0.5 ms for the 32400 chunks of a 1080p frame, the whole C5 frame time)
-#ifndef RT_QUEUE_HEADS
-#define RT_QUEUE_HEADS 16
-#endif
-constexpr uint32_t kQueueCounters = RT_QUEUE_HEADS;  // <= 32: one word marks the exhausted heads
+constexpr uint32_t kQueueCounters = 16;  // <= 32: one word marks the exhausted heads (1-1024 heads measured)
 static_assert(kQueueCounters >= 1 && kQueueCounters <= 32, "queue heads");
 constexpr uint32_t kQueueAllDone = kQueueCounters == 32 ? 0xffffffffu : (1u << kQueueCounters) - 1u;
 
@@ -286,10 +260,7 @@ constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX
 // the first grows with the distance travelled, so the far side of every slab interval is widened by a
 // relative 2^-20 (≥ 2·(3·2^-24)): a box the exact ray meets is never culled, whatever the camera distance.
 // (Widening only adds box visits; the closest hit is decided by the exact primitive tests.)
-#ifndef RT_SLAB_SLACK  // A/B experiments: -DRT_SLAB_SLACK=1.0f disables the widening
-#define RT_SLAB_SLACK (1.0f + 0x1p-20f)
-#endif
-constexpr float kSlabSlack = RT_SLAB_SLACK;
+constexpr float kSlabSlack = 1.0f + 0x1p-20f;
 
 // Closest hit (BVHNode::Hit, Hittable.cuh:387-439, and the primitive tests of PerformHit :470-485).
 // Returns the primitive index (BVH order) or -1, and the hit distance in t_best.
@@ -1262,34 +1233,12 @@ typedef const __attribute__((address_space(4))) float ConstF32;
 typedef const __attribute__((address_space(4))) uint32_t ConstU32;
 typedef const __attribute__((address_space(4))) uint8_t ConstU8;
 typedef __attribute__((address_space(3))) uint16_t LdsU16;
-// Visit decision of the v3/v4 node loop: 2 = inline-asm lane-mask block with the "no leaf held" mask carried
-// in SGPRs through the visits (default: C2 −0.7 %, profiles/r02h_ab_asm_decide.txt), 1 = the same block with a
-// per-visit compare of `leaf`, 0 = the C++ statement of the decision (the specification of both)
-#ifndef RT_ASM_DECIDE
-#define RT_ASM_DECIDE 2
-#endif
-#ifndef RT_DIAG_NONE
-#define RT_DIAG_NONE 0
-#endif
-#ifndef RT_DIAG_OCT
-#define RT_DIAG_OCT 0
-#endif
-#ifndef RT_SLAB_ASM
-#define RT_SLAB_ASM 1
-#endif
 // v_min/v_max(3)_f32 as plain instructions: the operands are finite FMA results or canonical values
 __device__ __forceinline__ float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(a), "v"(b)); return r; }
 __device__ __forceinline__ float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
 __device__ __forceinline__ float vmax3(float a, float b, float c) { float r; asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
 __device__ __forceinline__ float vmin3(float a, float b, float c) { float r; asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
-#ifndef RT_PRIM_BUFFER
-#define RT_PRIM_BUFFER 1
-#endif
-constexpr uint32_t kPrimStep = RT_PRIM_BUFFER ? 32u : 1u;
-#ifndef RT_SCALAR_NODES
-#define RT_SCALAR_NODES 1
-#endif
-constexpr bool kScalarNodes = RT_SCALAR_NODES != 0;
+constexpr uint32_t kPrimStep = 32u;  // leaf cursor unit: bytes of one 32-B primitive record
 
 // Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
 // until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
@@ -1328,18 +1277,14 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         __builtin_amdgcn_make_buffer_rsrc((void*)nodes_tab, (short)48, 0x7fffffff, 0x00020000);
     constexpr uint32_t stk_off = STK_OFF / 2;  // in uint16 units
     const float tmin_s = kTmin;  // an SGPR operand of the slab test's v_max
-#if RT_PRIM_BUFFER
     const __amdgpu_buffer_rsrc_t prsrc = __builtin_amdgcn_make_buffer_rsrc((void*)prims, (short)0, 0x7fffffff, 0x00020000);
-#endif
     while (node != (uint32_t)kSentinel16 || leaf >= 0x8000u) {
         // t_best changes only in the leaf phase: canonicalised once here, not on every visit by fminf
         const float t_best_c = __builtin_canonicalizef(t_best);
         const uint32_t n_outer = COUNT_TESTS ? (uint32_t)__popcll(__ballot(1)) : 0u;  // lanes still tracing
         (void)n_outer;
-#if RT_ASM_DECIDE
-        // lanes holding no leaf yet (RT_ASM_DECIDE >= 2 carries it through the visits as an SGPR mask)
+        // lanes holding no leaf yet, carried through the visits as an SGPR mask
         uint64_t lzm = __ballot(leaf == 0);
-#endif
         while (node < (uint32_t)kSentinel16) {
             // the entry address as one v_lshl_add_u32 (LLVM emits a half-rate shift plus an add: C2 −0.2 %,
             // C3 −0.3 %, profiles/r02e_ab_stack_addr.txt)
@@ -1353,9 +1298,6 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             asm("" : "+v"(top1));
             asm("" : "+v"(top2));
             float c0min, c0max, c1min, c1max;
-#if RT_DIAG_NONE
-            float c0maxi = 0.0f, c1maxi = 0.0f;  // far distances without the t_best clip (diagnostic)
-#endif
             uint32_t ch0, ch1;
             // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0) for a
             // positive direction component and (0, 1/d) for a negative one,
@@ -1375,23 +1317,13 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 const float fy1 = __builtin_fmaf(n1.w, pa.y, __builtin_fmaf(n1.z, pc.y, -oi.y));
                 const float nz1 = __builtin_fmaf(n2.z, pa.z, __builtin_fmaf(n2.w, pc.z, -oi.z));
                 const float fz1 = __builtin_fmaf(n2.w, pa.z, __builtin_fmaf(n2.z, pc.z, -oi.z));
-#if RT_SLAB_ASM
                 // the plane distances are FMA results and t_best_c is canonical, so min/max need no
-                // canonicalising v_max (LLVM re-emits one per visit for a value carried into the loop)
+                // canonicalising v_max (LLVM re-emits one per visit for a value carried into the loop:
+                // C2 −1.8 %)
                 c0min = vmax3(nx0, ny0, vmax(tmin_s, nz0));
                 c0max = vmin3(fx0, fy0, vmin(fz0, t_best_c)) * kSlabSlack;
                 c1min = vmax3(nx1, ny1, vmax(tmin_s, nz1));
                 c1max = vmin3(fx1, fy1, vmin(fz1, t_best_c)) * kSlabSlack;
-#if RT_DIAG_NONE
-                c0maxi = vmin3(fx0, fy0, fz0) * kSlabSlack;
-                c1maxi = vmin3(fx1, fy1, fz1) * kSlabSlack;
-#endif
-#else
-                c0min = fmaxf(fmaxf(nx0, ny0), fmaxf(nz0, kTmin));
-                c0max = fminf(fminf(fx0, fy0), fminf(fz0, t_best_c)) * kSlabSlack;
-                c1min = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, kTmin));
-                c1max = fminf(fminf(fx1, fy1), fminf(fz1, t_best_c)) * kSlabSlack;
-#endif
             };
             if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
                 const uint32_t noff = (uint32_t)node << 6;
@@ -1403,7 +1335,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                      __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
             } else {  // 48 B of f32 boxes + 4 B of references
                 const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
-                if (kScalarNodes && __ballot(node != nu) == 0) {
+                if (__ballot(node != nu) == 0) {
                     // every active lane visits the same node: scalar loads through the constant cache, planes as
                     // SGPR operands of the FMAs — no vector-memory (TA/TD) traffic, the kernel's busiest unit
                     const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes_tab + nu * 48u);
@@ -1439,39 +1371,21 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 cnt.wnode += wave_leader();
                 if (__ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0) cnt.wnode_uniform += wave_leader();
                 const uint32_t act = (uint32_t)__popcll(__ballot(1));
-#if RT_DIAG_OCT
-                // diagnostic build: counter 13 = node iterations whose tracing lanes share one direction octant,
-                // 14 = ... and one node (the scalar path)
-                {
-                    const uint32_t oct = (rd.x < 0.0f ? 1u : 0u) | (rd.y < 0.0f ? 2u : 0u) | (rd.z < 0.0f ? 4u : 0u);
-                    const bool oct_uniform = __ballot(oct != (uint32_t)__builtin_amdgcn_readfirstlane(oct)) == 0;
-                    const bool node_uniform = __ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0;
-                    if (wave_leader()) {
-                        cnt.idle_nt += oct_uniform ? 1u : 0u;
-                        cnt.idle_fin += (oct_uniform && node_uniform) ? 1u : 0u;
-                    }
-                }
-#elif RT_DIAG_NONE
-                // diagnostic build: counters 13/14 = visits whose two children both miss / ... that would be
-                // hit without the t_best clip (the visits a popped-entry distance test could skip)
-                {
-                    const bool nn = !(c0min <= c0max) && !(c1min <= c1max);
-                    cnt.idle_nt += nn ? 1u : 0u;
-                    cnt.idle_fin += (nn && (c0min <= c0maxi || c1min <= c1maxi)) ? 1u : 0u;
-                }
-                if (wave_leader()) cnt.idle_wait += n_outer - act;
-#else
                 if (wave_leader()) {
                     cnt.idle_nt += 64u - ntrav;
                     cnt.idle_fin += ntrav - n_outer;
                     cnt.idle_wait += n_outer - act;
                 }
-#endif
             }
-#if RT_ASM_DECIDE
-            // The visit decision as one block of lane-mask arithmetic: the hit / order / leaf masks stay in SGPR
-            // pairs (SALU combines them), one compare of `leaf` serves both the postpone decision and the exit
-            // mask, and the exit test needs no VALU materialisation of a ballot.  Same results as the C++ below.
+            // The visit decision as one block of lane-mask arithmetic (C2 −0.7 % against its C++ statement,
+            // profiles/r02h_ab_asm_decide.txt): the hit / order / leaf masks stay in SGPR pairs (SALU combines
+            // them), the "no leaf held yet" mask is carried in SGPRs through the visits, and the exit test needs
+            // no VALU materialisation of a ballot.  In C++ terms, with h0/h1 = child hit, swap = c1min < c0min:
+            //   both = h0 && h1, none = !(h0 || h1); near = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
+            //   far = swap ? ch0 : ch1 is written at the stack top unconditionally (kept when both);
+            //   next = none ? top1 : near; sp += both - none (the sentinel pads make an empty pop yield the
+            //   sentinel); a first leaf (next >= 0x8000 with no leaf held) is postponed: leaf = next and
+            //   next = the new stack top (both ? far : none ? top2 : top1), sp -= 1.
             {
                 uint32_t farc, xr, nxt, at;
                 uint64_t m0, m1, m2, m3, m4, m5;
@@ -1492,19 +1406,13 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     "s_not_b64 %[m0], %[m0]\n\t"                      // none
                     "v_subb_co_u32 %[sp], %[m3], %[sp], 0, %[m0]\n\t"  // pop
                     "v_cmp_lt_u32 %[m1], %[sent], %[nxt]\n\t"         // next is a leaf
-#if RT_ASM_DECIDE >= 2
                     "s_mov_b64 %[m4], %[lzm]\n\t"                     // no leaf held yet (carried mask)
-#else
-                    "v_cmp_eq_u32 %[m4], 0, %[leaf]\n\t"              // no leaf held yet
-#endif
                     "s_and_b64 %[m1], %[m1], %[m4]\n\t"               // postpone
                     "v_cndmask_b32 %[leaf], %[leaf], %[nxt], %[m1]\n\t"
                     "v_cndmask_b32 %[node], %[nxt], %[at], %[m1]\n\t"
                     "v_subb_co_u32 %[sp], %[m3], %[sp], 0, %[m1]\n\t"  // pop the entry under the postponed leaf
                     "s_andn2_b64 %[m5], %[m4], %[m1]\n\t"             // lanes still without a leaf
-#if RT_ASM_DECIDE >= 2
                     "s_mov_b64 %[lzm], %[m5]\n\t"
-#endif
                     "s_and_b64 %[m5], %[m5], exec"
                     : [farc] "=&v"(farc), [xr] "=&v"(xr), [nxt] "=&v"(nxt), [at] "=&v"(at), [node] "=&v"(node),
                       [sp] "+v"(sp), [leaf] "+v"(leaf), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
@@ -1514,29 +1422,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                 (void)m0; (void)m2; (void)m3;
                 *sp_entry = (uint16_t)farc;
                 if (m5 == 0) break;
-                continue;
             }
-#endif
-            const bool h0 = c0min <= c0max;
-            const bool h1 = c1min <= c1max;
-            const bool swap = c1min < c0min;
-            const bool both = h0 && h1, none = !(h0 || h1);
-            const uint32_t nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
-            const uint32_t farc = swap ? ch0 : ch1;
-            *sp_entry = (uint16_t)farc;
-            uint32_t nxt = none ? top1 : nearc;
-            // no underflow guards: the two sentinel pads below kStackBase make a pop of the empty stack
-            // yield kSentinel16, which ends this lane's traversal before sp can drop further
-            uint32_t nsp = sp + (both ? 1u : 0u) - (none ? 1u : 0u);
-            // first leaf: postpone it and pop the next entry (the stack top after this visit)
-            const bool postpone = nxt >= 0x8000u && leaf == 0;
-            const uint32_t after_top = both ? farc : (none ? top2 : top1);
-            leaf = postpone ? nxt : leaf;
-            nxt = postpone ? after_top : nxt;
-            nsp = postpone ? nsp - 1u : nsp;
-            node = nxt;
-            sp = nsp;
-            if (__ballot(leaf == 0) == 0) break;
         }
         const uint64_t t_leaf = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         // One primitive per lane per iteration: a lane walks its leaf's primitives and then the leaves
@@ -1552,15 +1438,10 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         while (cur < end) {
             {
                 const uint32_t i = cur / kPrimStep;  // the primitive's index (a shift, needed only on a hit)
-#if RT_PRIM_BUFFER
                 // byte offsets through a buffer descriptor: no 64-bit address arithmetic per primitive, and
                 // two 16-B loads (two texture-addresser requests) per test
                 const float4 p0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, cur, 0, 0));
                 const float4 p1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, cur + 16u, 0, 0));
-#else
-                const float4 p0 = prims[2 * i + 0];
-                const float4 p1 = prims[2 * i + 1];
-#endif
                 const uint32_t type = __float_as_uint(p1.w) & 15u;
                 if (COUNT_TESTS) {
                     cnt.prims++;
@@ -2022,12 +1903,8 @@ KernelFn v4_pick(bool count, bool tex) {
     return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH> : dev::render_kernel_v4<false, false, dev::NODES_64, PH>;
 }
 
-#ifndef RT_XORWOW_COMPACT_W  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
-#define RT_XORWOW_COMPACT_W 8
-#endif
-#ifndef RT_PHILOX_COMPACT_W  // __launch_bounds__ waves per SIMD of the non-texture Philox build of variant 3
-#define RT_PHILOX_COMPACT_W 7
-#endif
+constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
+constexpr int kPhiloxCompactWaves = 7;  // ... of the non-texture Philox build of variant 3
 
 KernelFn pick(int variant, bool count, bool tex, bool philox) {
     switch (variant) {
@@ -2039,8 +1916,8 @@ KernelFn pick(int variant, bool count, bool tex, bool philox) {
         // 28 B of cold spills) 16.98 vs 17.25 ms at the compiler's 68; Philox held to 72 (7 waves) 21.5 vs
         // 21.9 ms at 75, while 8 waves (64 VGPRs, 40 B of spills) ran 22.6 ms
         if (philox)
-            return tex ? v3_pick<1, true, true>(count, true) : v3_pick<RT_PHILOX_COMPACT_W, true, true>(count, false);
-        return tex ? v3_pick<1, false, true>(count, true) : v3_pick<RT_XORWOW_COMPACT_W, false, true>(count, false);
+            return tex ? v3_pick<1, true, true>(count, true) : v3_pick<kPhiloxCompactWaves, true, true>(count, false);
+        return tex ? v3_pick<1, false, true>(count, true) : v3_pick<kXorwowCompactWaves, false, true>(count, false);
     default: return philox ? v4_pick<true>(count, tex) : v4_pick<false>(count, tex);
     }
 }
