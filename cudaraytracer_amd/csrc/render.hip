@@ -203,12 +203,16 @@ struct KParams {
     float k10_fwd[3];  // (1.0f / inputs.fov * 10.0f) * forwardV (Kernel.cu:143)
     float bg0[3], bg1[3];
     uint32_t regen_threshold;  // v2: lanes still tracing below which finished lanes are regenerated
-    uint32_t* work_counter;    // v4: the frame's kQueueCounters queue heads, 128 B apart (zeroed before the launch)
+    uint32_t* work_counter;    // v4: the frame's kQueueCounters queue heads, queue_stride words apart (zeroed before
+                               // the launch), then the exhausted-heads word
+    uint32_t queue_stride;     // v4: words between queue heads (RT_TUNE_QUEUE_STRIDE; 32 = 128 B)
+    uint32_t work_chunk;       // v4: work indices a wave takes per atomic (RT_TUNE_QUEUE_CHUNK; a multiple of 64)
     uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
-    uint32_t work_per_counter; // v4: indices per queue head (a multiple of 64): head k owns [k·n, (k+1)·n)
+    uint32_t work_per_counter; // v4: indices per queue head (a multiple of work_chunk): head k owns [k·n, (k+1)·n)
     uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
     uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
-    unsigned long long* wave_trace;  // diagnostic (v3): per tile {start, end} of s_memrealtime (100 MHz)
+    unsigned long long* wave_trace;  // diagnostic: v3 per tile {start, end}; v4 per wave {start, queue drained,
+                                     // end, pixels} of s_memrealtime (100 MHz)
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
@@ -1666,6 +1670,8 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     uint32_t qc = blockIdx.x % kQueueCounters, qtried = 0u;
     uint32_t wave_pixels = 0u;           // wave-uniform: pixels this wave has taken
     const uint32_t threshold = P.regen_threshold;
+    const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+    uint64_t rt_drained = 0u;
 
     while (true) {
         if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
@@ -1705,17 +1711,18 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                 if (wq_next >= wq_end) {
                     const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
                     uint32_t base = 0u;
-                    if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * 32u, 64u);
+                    if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, P.work_chunk);
                     base = __builtin_amdgcn_readlane(base, leader);
                     const uint32_t idx = qc * P.work_per_counter + base;
                     if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
                         // mark it in the exhausted-heads word and move to the next live head (so a wave
                         // probes a few heads at the frame's end, not every one of them)
                         uint32_t done = 0u;
-                        if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * 32u, 1u << qc);
+                        if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * P.queue_stride, 1u << qc);
                         done = __builtin_amdgcn_readlane(done, leader) | (1u << qc);
                         if (done == kQueueAllDone || ++qtried >= kQueueCounters) {
                             drained = true;
+                            if (P.wave_trace) rt_drained = __builtin_amdgcn_s_memrealtime();
                             break;
                         }
                         const uint32_t live = ~done & kQueueAllDone;        // (nonzero here)
@@ -1724,7 +1731,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                         continue;
                     }
                     wq_next = idx;
-                    wq_end = idx + 64u;
+                    wq_end = idx + P.work_chunk;
                 }
                 const uint32_t avail = wq_end - wq_next;
                 const uint32_t rank =
@@ -1764,6 +1771,13 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     cnt.rays = park[PK_RAYS * 64];
     // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
     cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;
+    if (P.wave_trace && wave_leader()) {  // ramp / steady state / tail of the persistent grid (tools/v4_timeline.py)
+        unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
+        w[0] = rt_start;
+        w[1] = rt_drained;
+        w[2] = __builtin_amdgcn_s_memrealtime();
+        w[3] = wave_pixels;
+    }
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
@@ -2016,11 +2030,14 @@ thread_local int g_persistent_waves = 0;  // 0: occupancy query
 constexpr size_t kLdsLimit = 160 * 1024;
 
 // Work-queue heads of the persistent kernel: a ring of counters per device, one slot per launch, zeroed
-// on the launch's stream right before it.  A slot is kQueueBytes (the kQueueCounters heads 128 B apart plus
-// the exhausted-heads word) and is reused after kQueueSlots further persistent launches on that device: a
-// caller may keep at most kQueueSlots persistent launches in flight per device (rt_hip.h, rt_render).
+// on the launch's stream right before it.  A slot is kQueueBytes (the kQueueCounters heads, up to 4 KB apart,
+// plus the exhausted-heads word) and is reused after kQueueSlots further persistent launches on that device:
+// a caller may keep at most kQueueSlots persistent launches in flight per device (rt_hip.h, rt_render).
 constexpr uint32_t kQueueSlots = 256;
-constexpr uint32_t kQueueBytes = (dev::kQueueCounters + 1u) * 128u;  // one launch's heads + exhausted-heads word
+constexpr uint32_t kQueueMaxStride = 4096;  // bytes between heads (RT_TUNE_QUEUE_STRIDE)
+constexpr uint32_t kQueueBytes = (dev::kQueueCounters + 1u) * kQueueMaxStride;
+thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 queue heads
+thread_local int g_queue_chunk = 64;    // RT_TUNE_QUEUE_CHUNK: work indices per queue atomic
 constexpr int kMaxDevices = 64;
 struct QueueRing {
     uint32_t* buf = nullptr;
@@ -2144,6 +2161,24 @@ int rt_set_tuning(int key, int value) {
         }
         int prev = g_lds_pad;
         g_lds_pad = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_CHUNK) {
+        if (value < 64 || value > 4096 || value % 64) {
+            set_error("rt_set_tuning: queue chunk must be a multiple of 64 in [64, 4096]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_chunk;
+        g_queue_chunk = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_STRIDE) {
+        if (value < 128 || value > (int)kQueueMaxStride || (value & (value - 1))) {
+            set_error("rt_set_tuning: queue head stride must be a power of two in [128, 4096] bytes");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_stride;
+        g_queue_stride = value;
         return prev;
     }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
@@ -2373,11 +2408,15 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                            "rt_render: occupancy query");
         if (rc != RT_OK) return rc;
         P.work_total = tiles * 64u;
-        P.work_per_counter = (tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
+        P.work_chunk = (uint32_t)g_queue_chunk;
+        P.queue_stride = (uint32_t)g_queue_stride / 4u;
+        P.work_per_counter = ((tiles * 64u + dev::kQueueCounters - 1u) / dev::kQueueCounters + P.work_chunk - 1u) /
+                             P.work_chunk * P.work_chunk;
         if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
         grid = (uint32_t)(resident < grid ? resident : grid);
-        rc = hip_check(hipMemsetAsync(P.work_counter, 0, kQueueBytes, s), "rt_render: work queue reset");
+        rc = hip_check(hipMemsetAsync(P.work_counter, 0, (size_t)(dev::kQueueCounters + 1u) * g_queue_stride, s),
+                       "rt_render: work queue reset");
         if (rc != RT_OK) return rc;
     }
     P.num_tiles = tiles;

@@ -279,8 +279,9 @@ float rt_last_kernel_ms(void);
  * any device update); < 0 before the first call. */
 float rt_last_launch_host_ms(void);
 
-/* Diagnostic (per thread): device buffer of 2 × uint64 per wave that later v3 launches fill with each wave's
- * start and end s_memrealtime (100 MHz) — occupancy/tail analysis (tools/wave_timeline.py).  NULL = off. */
+/* Diagnostic (per thread): device buffer that later launches fill with s_memrealtime stamps (100 MHz): v3,
+ * 2 × uint64 per 8×8 tile (its wave's start and end; tools/wave_timeline.py); v4, 4 × uint64 per persistent
+ * wave (start, the moment its work queue ran dry, end, pixels taken; tools/v4_timeline.py).  NULL = off. */
 int rt_set_wave_trace(void* buffer);
 
 /* Experiment (per thread): device uint32 permutation of the frame's 8×8 tiles giving the v3 kernels' launch
@@ -312,9 +313,12 @@ int rt_last_variant(void);
 /*   RT_TUNE_TEXEL_LAYOUT: device bytes per texel of the images of later rt_scene_create calls: 3 (default,
  *   the reference's RGB8 layout, Texture.cuh:76: three byte gathers per lookup) or 4 (RGBA8-padded: one dword
  *   gather per lookup, 4/3 the memory).  The image does not depend on it. */
+/*   RT_TUNE_QUEUE_CHUNK: work indices (pixels) a persistent (v4) wave takes from its queue head per atomic
+ *   (a multiple of 64 in [64, 4096], default 64).  RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's 16
+ *   queue heads (a power of two in [128, 4096], default 128).  Neither changes the image. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
-                     RT_TUNE_TEXEL_LAYOUT = 6 };
+                     RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

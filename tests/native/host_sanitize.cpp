@@ -218,6 +218,11 @@ static void outputs_and_misc() {
     CHECK(in.up[1] == -1.0f);
     CHECK(rt_set_tuning(99, 1) == RT_ERR_INVALID_ARGUMENT);
     CHECK(rt_set_tuning(RT_TUNE_TEXEL_LAYOUT, 5) == RT_ERR_INVALID_ARGUMENT);
+    CHECK(rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 96) == RT_ERR_INVALID_ARGUMENT);
+    CHECK(rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 192) == RT_ERR_INVALID_ARGUMENT);
+    CHECK(rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 8192) == RT_ERR_INVALID_ARGUMENT);
+    CHECK(rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 128) == 64 && rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 64) == 128);
+    CHECK(rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 4096) == 128 && rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 128) == 4096);
     CHECK(rt_render(nullptr, nullptr, nullptr) == RT_ERR_INVALID_ARGUMENT);
     const int dev0 = 0;
     rt_tiled_desc td{&dev0, 1, 16, 64, 32, 0, 0, 1984};

@@ -1,6 +1,7 @@
-"""profiles/pmc_c2_n1.json (read by bench.py) from tools/profile_pmc.sh runs of config 2 with the traffic
-groups (tools/pmc_groups_traffic.txt), one output directory per RNG mode, last (warm) dispatch of each pass.
-    python tools/pmc_bench_json.py <xorwow dir> <philox dir> [<xorwow soa-layout dir>] > profiles/pmc_c2_n1.json
+"""profiles/pmc_<config>_n1.json (read by bench.py) from tools/profile_pmc.sh runs of one config with the
+traffic groups (tools/pmc_groups_traffic.txt), one output directory per RNG mode, last (warm) dispatch of each pass.
+    python tools/pmc_bench_json.py [--config c2|c3|c5] <xorwow dir> <philox dir> [<xorwow soa-layout dir>]
+        > profiles/pmc_<config>_n1.json
 
 Derived fields (MI355X: 8 XCDs, 256 CUs, 1024 SIMDs; SQ_* counters aggregate over SEs, in quad-cycles):
   hbm_read_bytes_corrected = FETCH_SIZE (KB) x 1024 x 2   (gfx950 reports half of the wide reads,
@@ -9,10 +10,16 @@ Derived fields (MI355X: 8 XCDs, 256 CUs, 1024 SIMDs; SQ_* counters aggregate ove
   avg_waves_per_simd       = 4 SQ_WAVE_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8)
   valu_lane_utilization    = SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)
   ta_busy_frac_per_cu      = TA_TA_BUSY_sum / 256 / (GRBM_GUI_ACTIVE / 8)
-Algorithmic HBM bytes per pixel: XORWOW 24 B state in + 24 B out + 4 B RGBA8; Philox 4 B."""
+Algorithmic HBM bytes per pixel: XORWOW 24 B state in + 24 B out + 4 B RGBA8; Philox 4 B; config 5 (progressive)
+adds the float4 accumulator read and written (32 B)."""
 import collections, csv, glob, json, os, sys
 
-PIXELS = 1920 * 1080
+CONFIG = "c2"
+if len(sys.argv) > 2 and sys.argv[1] == "--config":
+    CONFIG = sys.argv[2]
+    del sys.argv[1:3]
+PIXELS = {"c2": 1920 * 1080, "c3": 3840 * 2160, "c5": 1920 * 1080}[CONFIG]
+ACCUM = 32 if CONFIG == "c5" else 0
 
 
 def passes(out):
@@ -46,7 +53,7 @@ def summary(out, rng):
         "hbm_read_bytes_corrected": read,
         "hbm_write_bytes": write,
         "hbm_bytes_per_launch": read + write,
-        "algorithmic_bytes_per_launch": PIXELS * (52 if rng == "xorwow" else 4),
+        "algorithmic_bytes_per_launch": PIXELS * ((52 if rng == "xorwow" else 4) + ACCUM),
         "valu_lane_utilization": round(p["SQ_THREAD_CYCLES_VALU"] / (64.0 * p["SQ_ACTIVE_INST_VALU"]), 4),
         "avg_waves_per_simd": round(4.0 * p["SQ_WAVE_CYCLES"] / (1024.0 * gui), 3),
         "ta_busy_frac_per_cu": round(p["TA_TA_BUSY_sum"] / 256.0 / gui, 4),
@@ -57,9 +64,10 @@ xorwow, philox = summary(sys.argv[1], "xorwow"), summary(sys.argv[2], "philox")
 soa = summary(sys.argv[3], "xorwow") if len(sys.argv) > 3 else None
 out = {
     "command": "rocprofv3 --pmc <one group per pass: FETCH_SIZE | WRITE_SIZE | SQ_* | TA_*> --kernel-include-regex "
-               "render_kernel -- python3 tools/one_frame.py --variant -1 --frames 3 [--rng philox | --state-layout soa]  "
-               "(tools/profile_pmc.sh, tools/pmc_groups_traffic.txt; config c2; last, warm dispatch; "
-               "tools/pmc_bench_json.py)",
+               f"render_kernel -- python3 tools/one_frame.py --config {CONFIG} --variant -1 --frames 3 [--rng philox | "
+               f"--state-layout soa]  (tools/profile_pmc.sh, tools/pmc_groups_traffic.txt; config {CONFIG}; last, warm "
+               "dispatch; tools/pmc_bench_json.py)",
+    "config": CONFIG,
     "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports 1/2 of wide reads). Algorithmic bytes: "
             "XORWOW mode 24 B state in + 24 B out + 4 B RGBA8 per pixel; the kernel touches 24 of each 48-B "
             "curandState (the reference layout), so whole lines move. Philox mode: 4 B per pixel; the 8x8 tile "
