@@ -58,8 +58,8 @@ static int upload(const std::vector<T>& host, void** dev, const char* what) {
 static void free_device(DeviceScene* s) {
     if (s->nodes) (void)hipFree((void*)s->nodes);
     if (s->nodes48) (void)hipFree((void*)s->nodes48);
-    if (s->refs16) (void)hipFree((void*)s->refs16);
-    s->nodes48 = s->refs16 = nullptr;
+    if (s->refs) (void)hipFree((void*)s->refs);
+    s->nodes48 = s->refs = nullptr;
     if (s->prims) (void)hipFree((void*)s->prims);
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);  // texels: owned by rt_scene::texel_block
@@ -79,8 +79,9 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.nodes = p;
     if ((rc = upload(h.nodes48, &p, "hipMalloc/hipMemcpy(nodes48)"))) goto fail;
     d.nodes48 = p;
-    if ((rc = upload(h.refs16, &p, "hipMalloc/hipMemcpy(refs16)"))) goto fail;
-    d.refs16 = p;
+    if ((rc = upload(h.refs, &p, "hipMalloc/hipMemcpy(refs)"))) goto fail;
+    d.refs = p;
+    d.wide_refs = h.wide_refs;
     if ((rc = upload(h.prims, &p, "hipMalloc/hipMemcpy(prims)"))) goto fail;
     d.prims = p;
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
@@ -100,7 +101,7 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;
-    d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs16.size() + h.prims.size() + h.mats.size()) * 4 +
+    d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs.size() + h.prims.size() + h.mats.size()) * 4 +
                      h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;

@@ -178,7 +178,7 @@ __device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
 struct KParams {
     const float4* nodes;
     const float4* nodes48;   // v3: three box float4 per node
-    const uint32_t* refs16;  // v3: packed 16-bit child references
+    const uint32_t* refs;    // v3: child references per node: two 16-bit in one word, or (wide) two words
     const float4* prims;
     const float4* mats;
     const int4* imgs;
@@ -1108,13 +1108,23 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
 //     depth counters) is parked in LDS while the lane traverses, and the ray's reciprocal direction /
 //     |d|² are recomputed on entry to the traversal phase: only the ray, the traversal cursor and the
 //     closest hit stay in VGPRs across phases;
-//   * 16-bit traversal stack entries in LDS (node and leaf references fit a signed 16 bits when the
-//     scene has < 32767 nodes and < 8192 primitives; rt_render falls back to v2 otherwise);
+//   * 16-bit traversal stack entries in LDS when node and leaf references fit a signed 16 bits (the scene
+//     has < 32767 nodes and < 8192 primitives), 32-bit ones otherwise (WIDE instantiations, RefW below);
 //   * the lane's ray count is parked with the path state; primary samples = spp per pixel.
 // LDS per wave: 15 × 256 B of parked state + (depth + 2) × 128 B of stack (2 sentinel pads).
 // ---------------------------------------------------------------------------------------------------
-constexpr int kSentinel16 = 0x7fff;
 constexpr uint32_t kStackBase = 2;  // v3 stack entries start above two sentinel pads
+// Reference width of the v3/v4 kernels: 16-bit child and stack references (scenes with < 32767 nodes and < 8192
+// primitives: every BASELINE config), or 32-bit ones (WIDE: any scene the reference viewer can grow, AddHittable
+// CudaLayer.cpp:918-1370; 4-B LDS stack entries; the references' upper halves ride in the low bytes of the y
+// planes, scene_build.cpp).  References are unsigned in the width: internal nodes < kSentinel, leaves >= kLeaf.
+template <bool WIDE> struct RefW {
+    static constexpr uint32_t kSentinel = WIDE ? 0x7fffffffu : 0x7fffu;  // traversal finished
+    static constexpr uint32_t kLeaf = WIDE ? 0x80000000u : 0x8000u;      // references >= kLeaf are leaves
+    static constexpr uint32_t kMask = WIDE ? 0xffffffffu : 0xffffu;      // leaf ^ kMask = the leaf's ~ref
+    static constexpr uint32_t kLevelShift = WIDE ? 8u : 7u;              // log2(LDS bytes per stack level)
+    using Entry = typename std::conditional<WIDE, uint32_t, uint16_t>::type;
+};
 enum ParkSlot { PK_RNG = 0, PK_COL = 6, PK_ATT = 9, PK_SAMPLE = 12, PK_DEPTH = 13, PK_RAYS = 14, PK_WORDS = 15 };
 // Compact parking (v3, COMPACT): sample (13 bits), depth (6 bits) and the lane's ray count (13 bits) share
 // word PK_SD, so a wave parks 13 words instead of 15 — less LDS per wave, more resident waves (the v3
@@ -1131,18 +1141,19 @@ struct Cursor {
     int mode;
 };
 
+template <bool WIDE>
 __device__ __forceinline__ void v3_start_trace(uint32_t num_nodes, Cursor& c, uint32_t& rays) {
     rays++;
     c.t_best = FLT_MAX;
     c.hit = -1;
-    c.node = num_nodes ? 0 : kSentinel16;
+    c.node = num_nodes ? 0 : (int)RefW<WIDE>::kSentinel;
     c.leaf = 0;
     c.sp = kStackBase;
     c.mode = MODE_TRAV;
 }
 
 // A path ended with `contrib`: accumulate (Kernel.cu:147), then the next sample's camera ray, or finish.
-template <class R>
+template <bool WIDE, class R>
 __device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uint32_t g, f3 contrib, R& rng,
                                                f3& col, f3& att, uint32_t& sample, uint32_t& depth, f3& ro,
                                                f3& rd, Cursor& c, uint32_t& rays) {
@@ -1154,7 +1165,7 @@ __device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uin
         att = mk(1.0f, 1.0f, 1.0f);
         depth = 0;
         if (P.max_depth > 0) {
-            v3_start_trace(P.num_nodes, c, rays);
+            v3_start_trace<WIDE>(P.num_nodes, c, rays);
             return;
         }
         col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
@@ -1236,7 +1247,7 @@ __device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col,
 typedef const __attribute__((address_space(4))) float ConstF32;
 typedef const __attribute__((address_space(4))) uint32_t ConstU32;
 typedef const __attribute__((address_space(4))) uint8_t ConstU8;
-typedef __attribute__((address_space(3))) uint16_t LdsU16;
+template <class T> using Lds = __attribute__((address_space(3))) T;
 // v_min/v_max(3)_f32 as plain instructions: the operands are finite FMA results or canonical values
 __device__ __forceinline__ float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(a), "v"(b)); return r; }
 __device__ __forceinline__ float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
@@ -1247,14 +1258,16 @@ constexpr uint32_t kPrimStep = 32u;  // leaf cursor unit: bytes of one 32-B prim
 // Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
 // until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
 // still tracing (the wave then shades the finished lanes and regenerates them).
-template <bool COUNT_TESTS, int NODES, uint32_t STK_OFF>
-__device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, const __amdgpu_buffer_rsrc_t rrsrc,
-                                            const float4* __restrict__ nodes_tab, const uint32_t* __restrict__ refs16,
-                                            const float4* __restrict__ prims, int16_t* const stk,
+template <bool COUNT_TESTS, int NODES, uint32_t STK_OFF, bool WIDE>
+__device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
+                                            const float4* __restrict__ nodes_tab, const uint32_t* __restrict__ refs,
+                                            const float4* __restrict__ prims, typename RefW<WIDE>::Entry* const stk,
                                             const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
                                             Counts& cnt, const uint32_t ntrav = 64) {
-    // node / leaf references as unsigned 16-bit values: internal nodes < 0x7fff, kSentinel16 = 0x7fff, leaf
-    // references (int16 < 0 in the layout) >= 0x8000; leaf == 0: no postponed leaf
+    // node / leaf references as unsigned values of the reference width (RefW): internal nodes < kSentinel, leaf
+    // references (negative in the layout) >= kLeaf; leaf == 0: no postponed leaf
+    using RW = RefW<WIDE>;
+    using Entry = typename RW::Entry;
     uint32_t node = (uint32_t)c.node, leaf = (uint32_t)c.leaf;
     int hit = c.hit;
     uint32_t tag = c.tag;
@@ -1272,32 +1285,32 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     // changes only the sign of a zero plane distance, which no comparison sees)
     const f3 pa = mk(fmaxf(invd.x, 0.0f), fmaxf(invd.y, 0.0f), fmaxf(invd.z, 0.0f));
     const f3 pc = mk(fminf(invd.x, 0.0f), fminf(invd.y, 0.0f), fminf(invd.z, 0.0f));
-    const uint16_t* ustk = (const uint16_t*)stk;
+    const Entry* ustk = stk;
     // LDS address of this lane's stack entry 0 split into the lane part (VGPR) and the stack region's offset
     // STK_OFF (an immediate of the ds instructions)
-    const uint32_t stk_lane = (uint32_t)(uintptr_t)(LdsU16*)stk - STK_OFF;  // LDS base + the lane's 2-byte column
+    const uint32_t stk_lane = (uint32_t)(uintptr_t)(Lds<Entry>*)stk - STK_OFF;  // LDS base + the lane's column
     // structured (stride 48 B) view of the node boxes for the vector path's idxen loads
     const __amdgpu_buffer_rsrc_t rsrc_nodes_idx =
         __builtin_amdgcn_make_buffer_rsrc((void*)nodes_tab, (short)48, 0x7fffffff, 0x00020000);
-    constexpr uint32_t stk_off = STK_OFF / 2;  // in uint16 units
+    constexpr uint32_t stk_off = STK_OFF / sizeof(Entry);  // in entries
     const float tmin_s = kTmin;  // an SGPR operand of the slab test's v_max
     const __amdgpu_buffer_rsrc_t prsrc = __builtin_amdgcn_make_buffer_rsrc((void*)prims, (short)0, 0x7fffffff, 0x00020000);
-    while (node != (uint32_t)kSentinel16 || leaf >= 0x8000u) {
+    while (node != RW::kSentinel || leaf >= RW::kLeaf) {
         // t_best changes only in the leaf phase: canonicalised once here, not on every visit by fminf
         const float t_best_c = __builtin_canonicalizef(t_best);
         const uint32_t n_outer = COUNT_TESTS ? (uint32_t)__popcll(__ballot(1)) : 0u;  // lanes still tracing
         (void)n_outer;
         // lanes holding no leaf yet, carried through the visits as an SGPR mask
         uint64_t lzm = __ballot(leaf == 0);
-        while (node < (uint32_t)kSentinel16) {
+        while (node < RW::kSentinel) {
             // the entry address as one v_lshl_add_u32 (LLVM emits a half-rate shift plus an add: C2 −0.2 %,
             // C3 −0.3 %, profiles/r02e_ab_stack_addr.txt)
             uint32_t sa;
-            asm("v_lshl_add_u32 %0, %1, 7, %2" : "=v"(sa) : "v"(sp), "v"(stk_lane));
-            LdsU16* const sp_entry = (LdsU16*)(uintptr_t)sa + stk_off;
+            asm("v_lshl_add_u32 %0, %1, %3, %2" : "=v"(sa) : "v"(sp), "v"(stk_lane), "i"(RW::kLevelShift));
+            Lds<Entry>* const sp_entry = (Lds<Entry>*)(uintptr_t)sa + stk_off;
             uint32_t top1 = sp_entry[-64];
             uint32_t top2 = sp_entry[-128];
-            // materialise the zero-extended words here: used in another basic block, the loaded u16 would
+            // materialise the zero-extended words here: used in another basic block, a loaded u16 would
             // otherwise be re-extended there with a v_and per word and visit
             asm("" : "+v"(top1));
             asm("" : "+v"(top2));
@@ -1332,8 +1345,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
                 const uint32_t noff = (uint32_t)node << 6;
                 const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
-                ch0 = r2.x & 0xffffu;
-                ch1 = r2.y & 0xffffu;
+                ch0 = r2.x & RW::kMask;
+                ch1 = r2.y & RW::kMask;
                 slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
                      __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
                      __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
@@ -1343,9 +1356,15 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     // every active lane visits the same node: scalar loads through the constant cache, planes as
                     // SGPR operands of the FMAs — no vector-memory (TA/TD) traffic, the kernel's busiest unit
                     const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes_tab + nu * 48u);
-                    const uint32_t refs = *(const ConstU32*)((const ConstU8*)refs16 + nu * 4u);
-                    ch0 = refs & 0xffffu;
-                    ch1 = refs >> 16;
+                    if constexpr (WIDE) {
+                        const ConstU32* r = (const ConstU32*)((const ConstU8*)refs + nu * 8u);
+                        ch0 = r[0];
+                        ch1 = r[1];
+                    } else {
+                        const uint32_t r = *(const ConstU32*)((const ConstU8*)refs + nu * 4u);
+                        ch0 = r & 0xffffu;
+                        ch1 = r >> 16;
+                    }
                     slab(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
                          make_float4(cn[8], cn[9], cn[10], cn[11]));
                 } else {
@@ -1367,6 +1386,13 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                     // (a VOP3 takes no literal on gfx9: the selector is an SGPR operand)
                     asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch0) : "v"(n0.y), "v"(n0.x), "s"(0x0c0c0400u));
                     asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch1) : "v"(n1.y), "v"(n1.x), "s"(0x0c0c0400u));
+                    if constexpr (WIDE) {  // bits 16-31: byte 0 of lo_y | byte 0 of hi_y << 8, then the two halves
+                        uint32_t u0, u1;
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(u0) : "v"(n0.w), "v"(n0.z), "s"(0x0c0c0400u));
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(u1) : "v"(n1.w), "v"(n1.z), "s"(0x0c0c0400u));
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch0) : "v"(u0), "v"(ch0), "s"(0x05040100u));
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch1) : "v"(u1), "v"(ch1), "s"(0x05040100u));
+                    }
                     slab(n0, n1, n2);
                 }
             }
@@ -1422,9 +1448,9 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
                       [sp] "+v"(sp), [leaf] "+v"(leaf), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
                       [m3] "=&s"(m3), [m4] "=&s"(m4), [m5] "=&s"(m5), [lzm] "+s"(lzm)
                     : [a0] "v"(c0min), [b0] "v"(c0max), [a1] "v"(c1min), [b1] "v"(c1max), [ch0] "v"(ch0),
-                      [ch1] "v"(ch1), [t1] "v"(top1), [t2] "v"(top2), [sent] "s"(0x7fffu));
+                      [ch1] "v"(ch1), [t1] "v"(top1), [t2] "v"(top2), [sent] "s"(RW::kSentinel));
                 (void)m0; (void)m2; (void)m3;
-                *sp_entry = (uint16_t)farc;
+                *sp_entry = (Entry)farc;
                 if (m5 == 0) break;
             }
         }
@@ -1434,8 +1460,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
         // wave's longest leaf (same primitives in the same order per lane as a per-leaf loop).
         // cursor and end in units of kPrimStep (bytes of the 32-B primitive record with RT_PRIM_BUFFER)
         uint32_t cur = 0u, end = 0u;
-        if (leaf >= 0x8000u) {
-            const uint32_t l = leaf ^ 0xffffu;
+        if (leaf >= RW::kLeaf) {
+            const uint32_t l = leaf ^ RW::kMask;
             cur = (l >> 2) * kPrimStep;
             end = cur + ((l & 3u) + 1u) * kPrimStep;
         }
@@ -1493,9 +1519,9 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
             cur += kPrimStep;
             if (cur == end) {
                 leaf = 0;
-                if (node >= 0x8000u) {
+                if (node >= RW::kLeaf) {
                     leaf = node;
-                    const uint32_t l = leaf ^ 0xffffu;
+                    const uint32_t l = leaf ^ RW::kMask;
                     cur = (l >> 2) * kPrimStep;
                     end = cur + ((l & 3u) + 1u) * kPrimStep;
                     node = ustk[(sp - 1u) * 64];
@@ -1512,27 +1538,25 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc, 
     c.tag = tag;
     c.sp = sp;
     c.t_best = t_best;
-    if (c.node == kSentinel16 && c.leaf == 0) c.mode = MODE_SHADE;
+    if (node == RW::kSentinel && leaf == 0u) c.mode = MODE_SHADE;
 }
 
 // v3 kernel: one wave per workgroup, one 8×8 pixel tile per wave; LDS holds the wave's parked path state
 // and its traversal stacks (P.lds_wave_words words).
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false, bool COMPACT = false>
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false, bool COMPACT = false, bool WIDE = false>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    using Entry = typename RefW<WIDE>::Entry;
     constexpr int NODES = NODES_48;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t* const wl = (uint32_t*)lds;
     uint32_t* const park = wl + lane;                                                  // word k: park[k * 64]
-    int16_t* const stk = reinterpret_cast<int16_t*>(wl + park_words(COMPACT) * 64) + lane;  // stk[j * 64]
-    // node boxes and packed child references through buffer descriptors: 32-bit offsets, no 64-bit
-    // address arithmetic per visit; 48 B of boxes + 4 B of references per node
+    Entry* const stk = reinterpret_cast<Entry*>(wl + park_words(COMPACT) * 64) + lane;  // stk[j * 64]
+    // node boxes through a buffer descriptor: 32-bit offsets, no 64-bit address arithmetic per visit
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
                           : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rrsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
     const float4* __restrict__ prims = P.prims;
     uint32_t x, g;
     size_t pix;
@@ -1540,12 +1564,12 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     const uint32_t tile = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
     if (!lane_pixel<64>(P, x, g, pix, tile)) return;
     const bool rtl = P.rius_rtl != 0;
-    stk[0] = (int16_t)kSentinel16;  // two sentinel pads below the stack: popping an empty stack yields
-    stk[64] = (int16_t)kSentinel16;  // kSentinel16 without a bounds test
+    stk[0] = (Entry)RefW<WIDE>::kSentinel;   // two sentinel pads below the stack: popping an empty stack
+    stk[64] = (Entry)RefW<WIDE>::kSentinel;  // yields the sentinel without a bounds test
 
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
-    Cursor c{kSentinel16, 0, -1, 0u, 0u, FLT_MAX, MODE_DONE};
+    Cursor c{(int)RefW<WIDE>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_DONE};
 
     {  // first camera ray of the pixel
         uint32_t* st = state_at(P, pix);
@@ -1554,7 +1578,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         // (sample = -1: v3_next_sample starts sample 0; with spp = 0 it stays 0, so compact parking's packed
         // sample field cannot spill into the ray count)
         uint32_t sample = P.spp > 0 ? (uint32_t)-1 : 0u, depth = 0, rays = 0;
-        if (P.spp > 0) v3_next_sample(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
+        if (P.spp > 0) v3_next_sample<WIDE>(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
         v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);  // (col + 0 = +0 above)
     }
     const uint32_t threshold = P.regen_threshold;
@@ -1566,7 +1590,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt, ntrav);
+            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt, ntrav);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -1583,9 +1607,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
             if (ended) {
-                v3_next_sample(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
+                v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
             } else {
-                v3_start_trace(P.num_nodes, c, rays);
+                v3_start_trace<WIDE>(P.num_nodes, c, rays);
             }
             v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);
         }
@@ -1641,28 +1665,27 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
     return true;
 }
 
-template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false>
+template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false>
 __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    using Entry = typename RefW<WIDE>::Entry;
     extern __shared__ float4 lds[];
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t* const wl = (uint32_t*)lds;
     uint32_t* const park = wl + lane;
-    int16_t* const stk = reinterpret_cast<int16_t*>(wl + PK_WORDS4 * 64) + lane;
+    Entry* const stk = reinterpret_cast<Entry*>(wl + PK_WORDS4 * 64) + lane;
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
                           : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rrsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)P.refs16, (short)0, (int)(P.num_nodes * 4u), 0x00020000);
     const float4* __restrict__ prims = P.prims;
     const bool rtl = P.rius_rtl != 0;
-    stk[0] = (int16_t)kSentinel16;
-    stk[64] = (int16_t)kSentinel16;
+    stk[0] = (Entry)RefW<WIDE>::kSentinel;
+    stk[64] = (Entry)RefW<WIDE>::kSentinel;
     park[PK_RAYS * 64] = 0u;
 
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
-    Cursor c{kSentinel16, 0, -1, 0u, 0u, FLT_MAX, MODE_NEED};
+    Cursor c{(int)RefW<WIDE>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_NEED};
     uint32_t wq_next = 0u, wq_end = 0u;  // wave-uniform: the wave's current chunk of work indices
     bool drained = false;                // wave-uniform: the frame's queue is empty
     // wave-uniform: the queue head the wave draws from (one of kQueueCounters, each owning a contiguous
@@ -1674,7 +1697,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     uint64_t rt_drained = 0u;
 
     while (true) {
-        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u>(nrsrc, rrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs16, prims, stk, threshold, ro, rd, c, cnt);
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
         uint32_t sample, depth, rays;
@@ -1699,7 +1722,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                     fin = true;
                 }
             } else {
-                v3_start_trace(P.num_nodes, c, rays);
+                v3_start_trace<WIDE>(P.num_nodes, c, rays);
             }
         }
         // pixel regeneration: lanes without a pixel take the next work indices
@@ -1763,7 +1786,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
             camera_ray(q, cam_l, rng, ro, rd);
             att = mk(1.0f, 1.0f, 1.0f);
             depth = 0u;
-            v3_start_trace(P.num_nodes, c, rays);
+            v3_start_trace<WIDE>(P.num_nodes, c, rays);
         }
         if (shading || cam) v3_park(park, rng, col, att, sample, depth, rays);
         if (__ballot(c.mode != MODE_DONE) == 0) break;
@@ -1905,22 +1928,27 @@ constexpr Variant kVariants[] = {
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4;
 
-template <int W, bool PH = false, bool C = false>
+template <int W, bool PH = false, bool C = false, bool WD = false>
 KernelFn v3_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v3<true, W, true, PH, C> : dev::render_kernel_v3<false, W, true, PH, C>;
-    return count ? dev::render_kernel_v3<true, W, false, PH, C> : dev::render_kernel_v3<false, W, false, PH, C>;
+    if (tex) return count ? dev::render_kernel_v3<true, W, true, PH, C, WD> : dev::render_kernel_v3<false, W, true, PH, C, WD>;
+    return count ? dev::render_kernel_v3<true, W, false, PH, C, WD> : dev::render_kernel_v3<false, W, false, PH, C, WD>;
 }
 
-template <bool PH = false>
+template <bool PH = false, bool WD = false>
 KernelFn v4_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH> : dev::render_kernel_v4<false, true, dev::NODES_64, PH>;
-    return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH> : dev::render_kernel_v4<false, false, dev::NODES_64, PH>;
+    if (tex) return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH, WD> : dev::render_kernel_v4<false, true, dev::NODES_64, PH, WD>;
+    return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH, WD> : dev::render_kernel_v4<false, false, dev::NODES_64, PH, WD>;
 }
 
 constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
 constexpr int kPhiloxCompactWaves = 7;  // ... of the non-texture Philox build of variant 3
 
-KernelFn pick(int variant, bool count, bool tex, bool philox) {
+KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
+    if (wide) {  // 32-bit references: builds of the compact v3 and of v4 only (rt_render maps wide scenes there)
+        if (variant == kVarV3Compact)
+            return philox ? v3_pick<1, true, true, true>(count, tex) : v3_pick<1, false, true, true>(count, tex);
+        return philox ? v4_pick<true, true>(count, tex) : v4_pick<false, true>(count, tex);
+    }
     switch (variant) {
     case kVarV1: return count ? dev::render_kernel<true> : dev::render_kernel<false>;
     case kVarV2: return count ? dev::render_kernel_v2<true> : dev::render_kernel_v2<false>;
@@ -2224,7 +2252,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     std::memset(&P, 0, sizeof(P));
     P.nodes = (const float4*)S.nodes;
     P.nodes48 = (const float4*)S.nodes48;
-    P.refs16 = (const uint32_t*)S.refs16;
+    P.refs = (const uint32_t*)S.refs;
     P.prims = (const float4*)S.prims;
     P.mats = (const float4*)S.mats;
     P.imgs = (const int4*)S.imgs;
@@ -2352,25 +2380,27 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
             (void)hipGetLastError();  // (hipEventQuery reports hipErrorNotReady while pending)
         }
     }
-    const bool refs16_fit = S.num_nodes < (uint32_t)dev::kSentinel16 && S.num_prims < 8192u;
-    if (kVariants[variant].stack == dev::STACK_LDS16 && !refs16_fit) {
-        if (philox) {
-            set_error("rt_render: RT_FLAG_RNG_PHILOX needs the v3/v4 kernels (< 32767 BVH nodes, < 8192 primitives)");
-            return RT_ERR_UNSUPPORTED;
-        }
-        variant = S.depth <= 25u ? kVarV2 : kVarV1;  // 32-bit LDS stacks, or scratch if deep
-    }
     const bool packable =
         a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u;
     if (kVariants[variant].compact && !packable) variant = kVarV3;  // packed counters would overflow
     if (kVariants[variant].kernel == 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
-        variant = kVarV3;  // the persistent kernel assumes every pixel traces a ray
-    if (philox && kVariants[variant].stack != dev::STACK_LDS16) {
-        if (!refs16_fit) {
-            set_error("rt_render: RT_FLAG_RNG_PHILOX needs the v3/v4 kernels (< 32767 BVH nodes, < 8192 primitives)");
-            return RT_ERR_UNSUPPORTED;
+        variant = packable ? kVarV3Compact : kVarV3;  // the persistent kernel assumes every pixel traces a ray
+    if (philox && kVariants[variant].stack != dev::STACK_LDS16)
+        variant = packable ? kVarV3Compact : kVarV3;  // the v1/v2 kernels have no Philox build
+    // Scenes whose references need 32 bits (S.wide_refs: >= 32767 nodes or >= 8192 primitives) run the WIDE builds
+    // of the compact v3 and of v4; the 15-word v3 has none: v2 / v1 there (no Philox build either).
+    bool wide = false;
+    if (kVariants[variant].stack == dev::STACK_LDS16 && S.wide_refs) {
+        if (variant == kVarV3) {
+            if (philox) {
+                set_error("rt_render: RT_FLAG_RNG_PHILOX on a scene with 32-bit references needs spp < 8192, "
+                          "max_depth < 64 and spp * max_depth < 8192");
+                return RT_ERR_UNSUPPORTED;
+            }
+            variant = S.depth <= 25u ? kVarV2 : kVarV1;  // 32-bit LDS stacks, or scratch if deep
+        } else {
+            wide = true;
         }
-        variant = packable ? kVarV3Compact : kVarV3;  // the v1/v2 fallbacks have no Philox build
     }
     const Variant& V = kVariants[variant];
     const bool persistent = V.kernel == 4;
@@ -2385,7 +2415,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // inside 10 × 512 B of LDS)
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
                                   ? (size_t)(persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
-                                        (size_t)(S.depth + 2) * 64 * 2 + (size_t)g_lds_pad
+                                        (size_t)(S.depth + 2) * 64 * (wide ? 4 : 2) + (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
     size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes;
@@ -2393,7 +2423,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
     }
-    KernelFn fn = pick(variant, count_tests, S.has_textures, philox);
+    KernelFn fn = pick(variant, count_tests, S.has_textures, philox, wide);
     const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave
     P.tiles_x = (a->width + tile - 1) / tile;
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);

@@ -51,8 +51,11 @@ constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) trave
 struct HostScene {
     std::vector<float> nodes;   // 16 floats per node
     std::vector<float> nodes48; // 12 floats per node: the three box float4 of `nodes` (v3 kernels), each child
-                                // reference also in the low bytes of its x planes (moved outward; scene_build.cpp)
-    std::vector<uint32_t> refs16;  // per node: child 0 | child 1 << 16 as signed 16-bit references
+                                // reference also in the low bytes of its x planes (and, wide, of its y planes;
+                                // moved outward; scene_build.cpp)
+    std::vector<uint32_t> refs;    // per node: child 0 | child 1 << 16 as 16-bit references, or (wide_refs) the
+                                   // two 32-bit references
+    bool wide_refs = false;        // references need 32 bits: >= 32767 nodes or >= 8192 primitives
     std::vector<float> prims;   // 8 floats per primitive
     std::vector<float> mats;    // 12 floats per material
     std::vector<int32_t> imgs;  // 4 ints per image

@@ -11,7 +11,8 @@ namespace rt {
 struct DeviceScene {
     const void* nodes = nullptr;   // float4 × 4 per node
     const void* nodes48 = nullptr; // float4 × 3 per node (boxes only)
-    const void* refs16 = nullptr;  // uint32 per node: two signed 16-bit child references
+    const void* refs = nullptr;    // per node: uint32 of two 16-bit child references, or (wide_refs) two uint32
+    bool wide_refs = false;
     const void* prims = nullptr;   // float4 × 2 per primitive
     const void* mats = nullptr;    // float4 × 3 per material
     const void* imgs = nullptr;    // int4 per image

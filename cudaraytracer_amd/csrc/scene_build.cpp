@@ -350,6 +350,12 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         p.src = (int)i;
         B.prims.push_back(p);
     }
+    // the kernels address primitives as 32-B records at 32-bit byte offsets, and leaf references hold
+    // first << 2 in a signed 32-bit value
+    if (B.prims.size() >= ((size_t)1 << 26)) {
+        *err = "more than 2^26 active primitives";
+        return RT_ERR_INVALID_SCENE;
+    }
     B.traversal = (float)g_sah_traversal_x10 / 10.0f;
     B.build_root();
     // Occupancy guard: a tree deeper than kOccupancyDepth costs the compact v3 kernel its 8th wave per SIMD (its
@@ -384,22 +390,35 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         o[14] = 0.0f;
         o[15] = 0.0f;
     }
+    // 16-bit references (internal nodes < 0x7fff, leaves ~(first << 2 | count - 1) with first < 8192) unless the
+    // tree is too large: then 32-bit ones (the kernels' WIDE builds, render.hip RefW)
+    out->wide_refs = !(out->num_nodes < 0x7fffu && out->num_prims < 8192u);
     out->nodes48.resize((size_t)out->num_nodes * 12);
-    out->refs16.resize(out->num_nodes);
+    out->refs.resize((size_t)out->num_nodes * (out->wide_refs ? 2 : 1));
     for (uint32_t i = 0; i < out->num_nodes; i++) {
         float* o48 = out->nodes48.data() + (size_t)i * 12;
         for (int k = 0; k < 12; k++) o48[k] = out->nodes[(size_t)i * 16 + k];
         const Builder::Node& n = B.nodes[i];
-        const uint32_t r = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);  // valid when refs fit int16
-        out->refs16[i] = r;
-        // The two 16-bit child references also ride in the low bytes of the x planes (lo_x, hi_x of each child),
-        // so a lane's three 16-B box loads carry them and the vector path needs no fourth load (render.hip).
-        // Each carrier plane moves outward by < 512 ulps (lo down, hi up): the box only grows, and the culling
-        // stays conservative.
-        o48[0] = with_low_byte(o48[0], r & 0xffu, false);
-        o48[1] = with_low_byte(o48[1], (r >> 8) & 0xffu, true);
-        o48[4] = with_low_byte(o48[4], (r >> 16) & 0xffu, false);
-        o48[5] = with_low_byte(o48[5], r >> 24, true);
+        // The child references also ride in the low bytes of the planes (lo_x, hi_x of each child: bits 0-15;
+        // wide: lo_y, hi_y: bits 16-31), so a lane's three 16-B box loads carry them and the vector path needs
+        // no fourth load (render.hip).  Each carrier plane moves outward by < 512 ulps (lo down, hi up): the box
+        // only grows, and the culling stays conservative.
+        for (int c = 0; c < 2; c++) {
+            const uint32_t r = (uint32_t)n.child[c];
+            float* q = o48 + 4 * c;  // lo_x, hi_x, lo_y, hi_y of child c
+            q[0] = with_low_byte(q[0], r & 0xffu, false);
+            q[1] = with_low_byte(q[1], (r >> 8) & 0xffu, true);
+            if (out->wide_refs) {
+                q[2] = with_low_byte(q[2], (r >> 16) & 0xffu, false);
+                q[3] = with_low_byte(q[3], r >> 24, true);
+            }
+        }
+        if (out->wide_refs) {
+            out->refs[2 * (size_t)i] = (uint32_t)n.child[0];
+            out->refs[2 * (size_t)i + 1] = (uint32_t)n.child[1];
+        } else {
+            out->refs[i] = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);
+        }
     }
     out->prims.resize((size_t)out->num_prims * 8);
     out->prim_source.resize(out->num_prims);

@@ -165,6 +165,29 @@ CONFIGS = {
 }
 
 
+def sphere_field(n: int, seed: int) -> Scene:
+    """n small random spheres (Lambertian / metal / dielectric) over RTIOW's ground, under config 2's camera: the
+    large scenes the reference viewer grows with AddHittable (CudaLayer.cpp:918-1370)."""
+    rng = np.random.default_rng(seed)
+    h = (abi.HittableDesc * (n + 1))()
+    m = (abi.MaterialDesc * 4)()
+    for k, (t, f) in enumerate([(abi.RT_LAMBERTIAN, 0.0), (abi.RT_METAL, 0.3), (abi.RT_DIELECTRIC, 0.0),
+                                (abi.RT_LAMBERTIAN, 0.0)]):
+        m[k].type, m[k].fuzz, m[k].ir = t, f, 1.5
+        m[k].albedo.type, m[k].albedo.image = abi.RT_CONSTANT, -1
+        m[k].albedo.color[:] = [0.5, 0.6 - 0.1 * k, 0.3 + 0.1 * k]
+    h[0].type, h[0].is_active, h[0].material, h[0].radius = abi.RT_SPHERE, 1, 3, 1000.0
+    h[0].center[:] = [0.0, -1000.0, 0.0]
+    xyz = rng.uniform([-11.0, 0.05, -11.0], [11.0, 2.5, 11.0], (n, 3)).astype(np.float32)
+    rad = rng.uniform(0.03, 0.15, n).astype(np.float32)
+    mat = rng.integers(0, 3, n)
+    for i in range(n):
+        h[i + 1].type, h[i + 1].is_active = abi.RT_SPHERE, 1
+        h[i + 1].center[:] = [float(v) for v in xyz[i]]
+        h[i + 1].radius, h[i + 1].material = float(rad[i]), int(mat[i])
+    return Scene(h, m, [])
+
+
 def moving_camera(frame: int, frames: int = 60) -> tuple:
     """C5's scripted camera path: an orbit around the scene (position, orientation)."""
     ang = 2.0 * np.pi * frame / max(1, frames)

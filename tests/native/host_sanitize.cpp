@@ -275,7 +275,7 @@ static void node_reference_payload() {
             std::memcpy(&b[2], &q[4], 4);
             std::memcpy(&b[3], &q[5], 4);
             const uint32_t r = (b[0] & 0xffu) | ((b[1] & 0xffu) << 8) | ((b[2] & 0xffu) << 16) | ((b[3] & 0xffu) << 24);
-            CHECK(r == hs.refs16[i]);
+            CHECK(!hs.wide_refs && r == hs.refs[i]);
             for (int k : {0, 4}) CHECK(q[k] <= o[k] && o[k] - q[k] <= 512.0f * std::fabs(o[k]) * 0x1p-23f + 0x1p-140f);
             for (int k : {1, 5}) CHECK(q[k] >= o[k] && q[k] - o[k] <= 512.0f * std::fabs(o[k]) * 0x1p-23f + 0x1p-140f);
             for (int k : {2, 3, 6, 7, 8, 9, 10, 11}) CHECK(q[k] == o[k]);
@@ -283,6 +283,46 @@ static void node_reference_payload() {
         }
     }
     CHECK(checked > 250);  // RTIOW alone has 286 nodes
+    // a scene beyond 16-bit references (9000 primitives): 32-bit references, bits 16-31 in the y planes
+    {
+        const int n = 9000;
+        std::vector<rt_hittable_desc> h(n);
+        rt_material_desc mat{};
+        mat.type = RT_LAMBERTIAN;
+        mat.albedo.type = RT_CONSTANT;
+        mat.albedo.image = -1;
+        for (int i = 0; i < n; i++) {
+            h[i] = rt_hittable_desc{};
+            h[i].type = RT_SPHERE;
+            h[i].is_active = 1;
+            h[i].center[0] = (float)(i % 100) - 50.0f;
+            h[i].center[1] = 0.5f * (float)((i / 100) % 10);
+            h[i].center[2] = -(float)(i / 1000);
+            h[i].radius = 0.2f;
+        }
+        rt_scene_desc d{h.data(), (uint32_t)n, &mat, 1, nullptr, 0};
+        rt::HostScene hs;
+        std::string err;
+        CHECK(rt::build_host_scene(&d, &hs, &err, false) == RT_OK);
+        CHECK(hs.wide_refs && hs.refs.size() == 2 * (size_t)hs.num_nodes);
+        uint32_t leaves_beyond_16bit = 0;
+        for (uint32_t i = 0; i < hs.num_nodes; i++) {
+            const float* o = hs.nodes.data() + (size_t)i * 16;
+            const float* q = hs.nodes48.data() + (size_t)i * 12;
+            for (int c = 0; c < 2; c++) {
+                uint32_t b[4];
+                for (int k = 0; k < 4; k++) std::memcpy(&b[k], &q[4 * c + k], 4);
+                const uint32_t r = (b[0] & 0xffu) | ((b[1] & 0xffu) << 8) | ((b[2] & 0xffu) << 16) | ((b[3] & 0xffu) << 24);
+                uint32_t want;
+                std::memcpy(&want, &o[12 + c], 4);
+                CHECK(r == want && r == hs.refs[2 * (size_t)i + c]);
+                if ((int32_t)r < 0 && (~r >> 2) >= 8192u) leaves_beyond_16bit++;
+                for (int k : {0, 2}) CHECK(q[4 * c + k] <= o[4 * c + k]);
+                for (int k : {1, 3}) CHECK(q[4 * c + k] >= o[4 * c + k]);
+            }
+        }
+        CHECK(leaves_beyond_16bit > 0);
+    }
     // a box at the end of the float range: carrier planes stay finite
     rt_material_desc m{};
     m.type = RT_LAMBERTIAN;

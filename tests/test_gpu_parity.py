@@ -358,25 +358,7 @@ def test_scene_beyond_binary16_range_matches_oracle(variant):
 
 
 def _sphere_field(n: int, seed: int) -> scenes.Scene:
-    """n small random spheres (Lambertian / metal / dielectric) over RTIOW's ground, under config 2's camera."""
-    rng = np.random.default_rng(seed)
-    h = (abi.HittableDesc * (n + 1))()
-    m = (abi.MaterialDesc * 4)()
-    for k, (t, f) in enumerate([(abi.RT_LAMBERTIAN, 0.0), (abi.RT_METAL, 0.3), (abi.RT_DIELECTRIC, 0.0),
-                                (abi.RT_LAMBERTIAN, 0.0)]):
-        m[k].type, m[k].fuzz, m[k].ir = t, f, 1.5
-        m[k].albedo.type, m[k].albedo.image = abi.RT_CONSTANT, -1
-        m[k].albedo.color[:] = [0.5, 0.6 - 0.1 * k, 0.3 + 0.1 * k]
-    h[0].type, h[0].is_active, h[0].material, h[0].radius = abi.RT_SPHERE, 1, 3, 1000.0
-    h[0].center[:] = [0.0, -1000.0, 0.0]
-    xyz = rng.uniform([-11.0, 0.05, -11.0], [11.0, 2.5, 11.0], (n, 3)).astype(np.float32)
-    rad = rng.uniform(0.03, 0.15, n).astype(np.float32)
-    mat = rng.integers(0, 3, n)
-    for i in range(n):
-        h[i + 1].type, h[i + 1].is_active = abi.RT_SPHERE, 1
-        h[i + 1].center[:] = [float(v) for v in xyz[i]]
-        h[i + 1].radius, h[i + 1].material = float(rad[i]), int(mat[i])
-    return scenes.Scene(h, m, [])
+    return scenes.sphere_field(n, seed)
 
 
 @pytest.mark.parametrize("variant", [-1, 3, 4])
@@ -401,22 +383,55 @@ def test_large_scene_deep_bvh_matches_oracle(variant):
     assert int(r.counters[0]) == cnt.rays
 
 
-def test_scene_beyond_16bit_references_falls_back_and_matches_oracle():
-    """9000 spheres: leaf references no longer fit 16 bits, so the automatic choice falls back to the
-    32-bit-reference kernels (v2 / v1) — same image and ray count as the oracle."""
+@pytest.mark.parametrize("variant", [-1, 0, 1, 3, 4])
+def test_scene_beyond_16bit_references_matches_oracle(variant):
+    """9000 spheres: leaf references no longer fit 16 bits.  The automatic choice and variants 3 / 4 run the
+    32-bit-reference (WIDE) builds of v3 / v4; variants 0 / 1 the v1 / v2 kernels — all with the oracle's image
+    and ray count."""
     cfg = scenes.CONFIGS["c2"].scaled(64, 36, 2)
     sc = _sphere_field(9000, 6)
     ds = DeviceScene(sc)
-    lib().rt_set_variant(-1)
-    r = Renderer(cfg.width, cfg.height)
-    r.render_init()
-    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
-    torch.cuda.synchronize()
-    assert lib().rt_last_variant() in (0, 1)
+    assert ds.info().num_primitives == 9001
+    lib().rt_set_variant(variant)
+    try:
+        r = Renderer(cfg.width, cfg.height)
+        r.render_init()
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+        torch.cuda.synchronize()
+        assert lib().rt_last_variant() == (variant if variant >= 0 else lib().rt_last_variant())
+        assert lib().rt_last_variant() in ((3, 4) if variant < 0 else (variant,))
+    finally:
+        lib().rt_set_variant(-1)
     ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(),
                             po.init_states(cfg.width, cfg.height), threads=8)
     np.testing.assert_array_equal(r.image(), ref)
     assert int(r.counters[0]) == cnt.rays
+
+
+@pytest.mark.parametrize("variant, rng", [(3, "xorwow"), (4, "xorwow"), (3, "philox"), (4, "philox")])
+def test_20000_sphere_scene_wide_references_match_oracle(variant, rng):
+    """20 000 spheres (> 32767 BVH nodes would need ~3x that; here > 8191 leaves and primitives): the WIDE v3 / v4
+    builds, both RNG modes, bit-exact with the oracle (AddHittable grows scenes without limit,
+    CudaLayer.cpp:918-1370)."""
+    cfg = scenes.CONFIGS["c2"].scaled(48, 32, 2)
+    sc = _sphere_field(20000, 11)
+    ds = DeviceScene(sc)
+    lib().rt_set_variant(variant)
+    try:
+        r = Renderer(cfg.width, cfg.height, rng=rng)
+        r.render_init()
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), frame=1 if rng == "philox" else None)
+        torch.cuda.synchronize()
+        assert lib().rt_last_variant() == variant
+    finally:
+        lib().rt_set_variant(-1)
+    st = po.init_states(cfg.width, cfg.height) if rng == "xorwow" else None
+    ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                            threads=8, philox=rng == "philox", seed=1984, frame=1)
+    np.testing.assert_array_equal(r.image(), ref)
+    assert int(r.counters[0]) == cnt.rays
+    if rng == "xorwow":
+        np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -17,16 +17,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "cudaraytracer_amd", "librt_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
-# render_kernel_v3<COUNT_TESTS=false, W, TEX, PHILOX, COMPACT> (variants 2 and 3; the untextured compact builds
-# are held to 8 (XORWOW) / 7 (Philox) waves per SIMD by registers, render.hip RT_*_COMPACT_W)
-# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX> (variant 4)
-def _v3(t, p, c):
-    w = (8 if not p else 7) if (c and not t) else 1
-    return f"_ZN2rt3dev16render_kernel_v3ILb0ELi{w}ELb{t}ELb{p}ELb{c}EEEvNS0_7KParamsE"
+# render_kernel_v3<COUNT_TESTS=false, W, TEX, PHILOX, COMPACT, WIDE> (variants 2 and 3; the untextured compact
+# 16-bit-reference builds are held to 8 (XORWOW) / 7 (Philox) waves per SIMD by registers, render.hip
+# k*CompactWaves; the 32-bit-reference (WIDE) builds exist for the compact v3 and v4 only)
+# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX, WIDE> (variant 4)
+def _v3(t, p, c, wd=0):
+    w = (8 if not p else 7) if (c and not t and not wd) else 1
+    return f"_ZN2rt3dev16render_kernel_v3ILb0ELi{w}ELb{t}ELb{p}ELb{c}ELb{wd}EEEvNS0_7KParamsE"
 
 
-HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + \
-      [f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}EEEvNS0_7KParamsE" for t in (0, 1) for p in (0, 1)]
+def _v4(t, p, wd=0):
+    return f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}ELb{wd}EEEvNS0_7KParamsE"
+
+
+HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + [_v4(t, p) for t in (0, 1) for p in (0, 1)] + \
+      [_v3(t, p, 1, 1) for t in (0, 1) for p in (0, 1)] + [_v4(t, p, 1) for t in (0, 1) for p in (0, 1)]
 # register-held builds: a few bytes of cold spills (measured faster than the compiler's register count)
 SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 16}
 
@@ -58,7 +63,7 @@ def test_hot_kernels_register_and_scratch_budget(tmp_path):
     for k in HOT:
         assert k in meta, k
         assert meta[k]["private_segment_fixed_size"] <= SPILL_OK.get(k, 0), (k, meta[k])
-        if "render_kernel_v3ILb0ELi1ELb0ELb0E" in k:  # untextured XORWOW builds
+        if "render_kernel_v3ILb0ELi1ELb0ELb0E" in k or k == _v3(0, 0, 1):  # untextured XORWOW builds
             assert meta[k]["vgpr_count"] <= 72, (k, meta[k])
     # the default kernel of untextured many-sample frames (variant 3, XORWOW) at 8 waves per SIMD
     assert meta[_v3(0, 0, 1)]["vgpr_count"] <= 64
