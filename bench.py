@@ -89,6 +89,8 @@ def parse_args(argv=None):
                     help="rehearsal on a 1-GPU box: every rank renders on device 0 (use with --backend gloo)")
     ap.add_argument("--tiled-devices", default="",
                     help="single-process multi-device split through the rt_tiled C ABI, e.g. 0,1,2,3 (or 0,0 on one GPU)")
+    ap.add_argument("--no-config-lines", action="store_true",
+                    help="N=1 --config c2: skip the BASELINE config 3 and 5 figures attached to the headline line")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank launch: N gloo ranks gather synthetic bands (no GPU)")
     return ap.parse_args(argv)
@@ -273,7 +275,8 @@ def distinct_devices(world: int, device: int) -> int:
     return len(set(ids))
 
 
-def run_rank(args) -> None:
+def run_rank(args) -> dict | None:
+    """One rank's bench of args.config; returns rank 0's JSON line (None elsewhere)."""
     from cudaraytracer_amd import abi, scenes
     from cudaraytracer_amd._lib import lib
     from cudaraytracer_amd.renderer import DeviceScene, Renderer
@@ -411,9 +414,9 @@ def run_rank(args) -> None:
         if world == 1 and not args.no_cpu_baseline and not strong:
             cpu_inputs = inputs if not progressive else scenes.camera_inputs(*scenes.moving_camera(0, C5_FRAMES), cfg.fov)
             line["cpu_baseline"] = cpu_baseline(cfg, scene_desc, cpu_inputs, args.cpu_seconds)
-        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return line if rank == 0 else None
 
 
 def valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world) -> dict:
@@ -497,7 +500,20 @@ def main() -> None:
         from cudaraytracer_amd import scenes
         run_tiled(args, scenes.CONFIGS[args.config])
         return
-    run_rank(args)
+    line = run_rank(args)
+    if line is not None and args.config == "c2" and args.gpus == 1 and not args.no_config_lines:
+        # BASELINE configs 5 (the real-time progressive path) and 3 (Cornell, 256 spp) on the same run's clock
+        line["other_configs"] = {}
+        for name, steps, warmup in (("c5", 20, 3), ("c3", 2, 1)):
+            sub = argparse.Namespace(**vars(args))
+            sub.config, sub.steps, sub.warmup = name, steps, warmup
+            sub.no_cpu_baseline = sub.no_philox_line = True
+            o = run_rank(sub)
+            line["other_configs"][name] = {k: o[k] for k in ("metric", "value", "unit", "ms_per_step", "kernel_ms",
+                                                             "rays_per_frame", "steps", "warmup", "roofline")}
+            line["other_configs"][name]["workload"] = o["config"]["workload"]
+    if line is not None:
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
