@@ -160,7 +160,7 @@ template <class R> __device__ __forceinline__ void draw3(R& s, float& a, float& 
 // 2·ξ − 1 of each component with one fma: 2·ξ is exact, so it rounds like the reference's mul + sub.  The
 // fill order is two selects per attempt (a launch-uniform branch around the loop measured the same).
 template <class R>
-__device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
+__device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl, uint32_t* /*coop: Philox only*/) {
     f3 p;
     do {
         float a, b, c;
@@ -488,7 +488,7 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1 };
 template <bool TEX = true, class PP, class R>
 __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
-                                     f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
+                                     f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib, uint32_t* coop = nullptr) {
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
     // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
     // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
@@ -591,7 +591,7 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         ro = p;
         return SHADE_CONTINUE;
     }
-    const f3 q = random_in_unit_sphere(rng, rtl);
+    const f3 q = random_in_unit_sphere(rng, rtl, coop);
     const float4 m1 = P->mats[3 * mat + 1];
     f3 attenuation;
     bool ok = true;
@@ -768,10 +768,10 @@ struct RngPhilox {
     uint32_t k0, k1, frame;  // launch-uniform key and frame, read once when the stream is (un)parked
 };
 
-// Block `blk` of the lane's stream: philox10(ctr = {blk, frame, pixel, 0}, key = seed) into s.r0..r3.
-__device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
-    uint32_t c0 = blk, c1 = s.frame, c2 = s.pix, c3 = 0u;
-    uint32_t k0 = s.k0, k1 = s.k1;
+// philox10(ctr = {blk, frame, pixel, 0}, key = (k0, k1)) into w[0..3].
+__device__ __forceinline__ void philox10(uint32_t blk, uint32_t frame, uint32_t pixel, uint32_t k0, uint32_t k1,
+                                         uint32_t* w) {
+    uint32_t c0 = blk, c1 = frame, c2 = pixel, c3 = 0u;
 #pragma unroll
     for (int i = 0; i < 10; i++) {  // single_round + bumpkey (rocrand_philox4x32_10.h:286-303)
         const uint64_t m0 = (uint64_t)0xD2511F53u * c0;  // one v_mad_u64_u32 for lo and hi
@@ -783,10 +783,20 @@ __device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
-    s.r0 = c0;
-    s.r1 = c1;
-    s.r2 = c2;
-    s.r3 = c3;
+    w[0] = c0;
+    w[1] = c1;
+    w[2] = c2;
+    w[3] = c3;
+}
+
+// Block `blk` of the lane's stream into s.r0..r3.
+__device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
+    uint32_t w[4];
+    philox10(blk, s.frame, s.pix, s.k0, s.k1, w);
+    s.r0 = w[0];
+    s.r1 = w[1];
+    s.r2 = w[2];
+    s.r3 = w[3];
 }
 
 __device__ __forceinline__ float philox_to_uniform(uint32_t x) {
@@ -835,6 +845,141 @@ __device__ __forceinline__ void draw3(RngPhilox& s, float& a, float& b, float& c
     a = philox_to_uniform(w[0]);
     b = philox_to_uniform(w[1]);
     c = philox_to_uniform(w[2]);
+}
+
+// RandomInUnitSphere (Math.cuh:252-260) on a Philox stream, wave-cooperatively.  The rejection loop runs until
+// the wave's last sampling lane accepts (~6 iterations for ~40 lanes at acceptance pi/6), and every iteration in
+// which some lane needs a new block pays a whole-wave Philox evaluation (~160 issue cycles) for a few live lanes.
+// A Philox block is a pure function of (pixel, block index), so lanes that have accepted can generate and test
+// the blocks of those still looping: once at most min(16, A/2) of the A sampling lanes are still looping, each of
+// them gets m = A / k helpers; helper `slot` generates block (n >> 2) + slot of its owner's stream, fetches the next
+// helper's block (ds_bpermute) and evaluates the attempts that start in its block; the owner takes the first
+// accepting attempt (an LDS atomic min over attempt indices) or, if none of the ~4m/3 attempts in its m blocks
+// accepts, skips them all.  Each attempt reads the same three words, in the same order, as the sequential loop,
+// so the accepted point and the stream position after it are the sequential loop's (bit-exact, the oracle's).
+// coop: per-wave LDS table of kCoopOwners entries (words: n, best attempt, pixel, point xyz, block of the
+// successor position); NULL runs the sequential loop.
+constexpr uint32_t kCoopOwners = 16;
+enum CoopWord { CO_N = 0, CO_BEST = 16, CO_PIX = 32, CO_P = 48, CO_BLK = 96, CO_WORDS = 160 };
+
+__device__ __forceinline__ f3 rius_point(uint32_t wa, uint32_t wb, uint32_t wc, bool rtl) {
+    const float a = philox_to_uniform(wa), b = philox_to_uniform(wb), c = philox_to_uniform(wc);
+    const f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
+    return mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
+}
+__device__ __forceinline__ bool rius_rejected(const f3 p) { return p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f; }
+
+__device__ __forceinline__ void lds_store(uint32_t* a, uint32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_load(uint32_t* a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wave_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__device__ __forceinline__ f3 random_in_unit_sphere(RngPhilox& s, bool rtl, uint32_t* coop) {
+    f3 p = mk(0.0f, 0.0f, 0.0f);
+    bool pending = true;
+    while (true) {
+        // attempts from the words left in the current block (no generation)
+        while (pending && (s.n & 3u) == 1u) {
+            const uint32_t wa = s.r1, wb = s.r2, wc = s.r3;
+            s.n += 3u;
+            p = rius_point(wa, wb, wc, rtl);
+            pending = rius_rejected(p);
+        }
+        const uint64_t pm = __ballot(pending);
+        if (pm == 0) break;
+        const uint64_t ex = __ballot(1);
+        const uint32_t A = (uint32_t)__popcll(ex), k = (uint32_t)__popcll(pm);
+        if (coop == nullptr || k > kCoopOwners || 2u * k > A) {  // many lanes still looping: each generates its own
+            if (pending) {
+                float a, b, c;
+                draw3(s, a, b, c);
+                const f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
+                p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
+                pending = rius_rejected(p);
+            }
+            continue;
+        }
+        // ---- cooperative round ----
+        const uint32_t lane = __lane_id();
+        const uint32_t h = __builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u));
+        const uint32_t orank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+        const uint32_t m = (uint32_t)(((float)A + 0.5f) / (float)k);  // helpers per owner (exact: A, k <= 64)
+        if (pending) {
+            lds_store(coop + CO_N + orank, s.n);
+            lds_store(coop + CO_BEST + orank, 0xffffffffu);
+            lds_store(coop + CO_PIX + orank, s.pix);
+        }
+        wave_order();
+        const uint32_t rr = (uint32_t)(((float)h + 0.5f) / (float)m);  // the owner rank this lane helps
+        const uint32_t slot = h - rr * m;
+        const bool helper = rr < k;
+        const uint32_t n_o = helper ? lds_load(coop + CO_N + rr) : 0u;
+        const uint32_t opix = helper ? lds_load(coop + CO_PIX + rr) : 0u;
+        const uint32_t b0 = n_o >> 2, j = n_o & 3u;
+        uint32_t w[4], x[2];
+        philox10(b0 + slot, s.frame, opix, s.k0, s.k1, w);
+        // the next block of the owner's stream is the next active lane's (the next helper slot)
+        const uint64_t above = ex & ~((2ull << lane) - 1ull);
+        const uint32_t nl = above ? (uint32_t)__builtin_ctzll(above) : lane;
+#pragma unroll
+        for (int i = 0; i < 2; i++) x[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nl << 2), (int)w[i]);
+        const bool nvalid = slot + 1u < m;
+        // attempts starting in this block: a1 (offset o1) and, when o1 == 0, a1 + 1 (words 3, 4, 5)
+        const int t = (int)(4u * slot) - (int)j;
+        const uint32_t a1 = t <= 0 ? 0u : ((uint32_t)t + 2u) / 3u;
+        const uint32_t o1 = j + 3u * a1 - 4u * slot;  // 0..3
+        const uint32_t wa = o1 == 0u ? w[0] : (o1 == 1u ? w[1] : (o1 == 2u ? w[2] : w[3]));
+        const uint32_t wb = o1 == 0u ? w[1] : (o1 == 1u ? w[2] : (o1 == 2u ? w[3] : x[0]));
+        const uint32_t wc = o1 == 0u ? w[2] : (o1 == 1u ? w[3] : (o1 == 2u ? x[0] : x[1]));
+        const f3 p1 = rius_point(wa, wb, wc, rtl);
+        const f3 p2 = rius_point(w[3], x[0], x[1], rtl);
+        const bool v1 = helper && (o1 <= 1u || nvalid), v2 = helper && o1 == 0u && nvalid;
+        const bool acc1 = v1 && !rius_rejected(p1), acc2 = v2 && !rius_rejected(p2);
+        const uint32_t key = acc1 ? a1 : (acc2 ? a1 + 1u : 0xffffffffu);
+        const f3 pk = acc1 ? p1 : p2;
+        if (key != 0xffffffffu)
+            __hip_atomic_fetch_min(coop + CO_BEST + rr, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        wave_order();
+        const uint32_t best = helper ? lds_load(coop + CO_BEST + rr) : 0u;
+        // the owner's stream position after this round, and who holds the block it lies in
+        const uint32_t a_lim = (4u * m - j) / 3u;  // attempts wholly inside the owner's m blocks
+        const uint32_t n_next = best != 0xffffffffu ? n_o + 3u * best + 3u : n_o + 3u * a_lim;
+        const uint32_t nrel = (n_next >> 2) - b0;   // slot of the block holding n_next
+        if (helper && key != 0xffffffffu && key == best) {  // the winner publishes the point
+            lds_store(coop + CO_P + rr, __float_as_uint(pk.x));
+            lds_store(coop + CO_P + 16 + rr, __float_as_uint(pk.y));
+            lds_store(coop + CO_P + 32 + rr, __float_as_uint(pk.z));
+        }
+        // the block holding the successor position (needed unless it starts a block) is a helper's own: a winning
+        // attempt that crosses into the next block needs that block to be a helper slot of the same owner (nvalid)
+        if (helper && (n_next & 3u) != 0u && nrel == slot) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) lds_store(coop + CO_BLK + 16 * i + rr, w[i]);
+        }
+        wave_order();
+        if (pending) {
+            const uint32_t ob = lds_load(coop + CO_BEST + orank);
+            if (ob != 0xffffffffu) {
+                s.n += 3u * ob + 3u;
+                p = mk(__uint_as_float(lds_load(coop + CO_P + orank)), __uint_as_float(lds_load(coop + CO_P + 16 + orank)),
+                       __uint_as_float(lds_load(coop + CO_P + 32 + orank)));
+                pending = false;
+            } else {
+                s.n += 3u * ((4u * m - (s.n & 3u)) / 3u);  // all attempts in the owner's m blocks rejected
+            }
+            if ((s.n & 3u) != 0u) {
+                s.r0 = lds_load(coop + CO_BLK + orank);
+                s.r1 = lds_load(coop + CO_BLK + 16 + orank);
+                s.r2 = lds_load(coop + CO_BLK + 32 + orank);
+                s.r3 = lds_load(coop + CO_BLK + 48 + orank);
+            }
+        }
+        wave_order();
+    }
+    return p;
 }
 
 __device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPhilox&) {}  // stateless in HBM
@@ -1553,6 +1698,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     uint32_t* const wl = (uint32_t*)lds;
     uint32_t* const park = wl + lane;                                                  // word k: park[k * 64]
     Entry* const stk = reinterpret_cast<Entry*>(wl + park_words(COMPACT) * 64) + lane;  // stk[j * 64]
+    // Philox: the cooperative sampler's table at the end of the wave's LDS
+    uint32_t* const coop = PHILOX ? wl + P.lds_wave_words - CO_WORDS : nullptr;
     // node boxes through a buffer descriptor: 32-bit offsets, no 64-bit address arithmetic per visit
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
@@ -1601,7 +1748,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib,
+                                    coop) == SHADE_ENDED;
             if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
@@ -1674,6 +1822,7 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     uint32_t* const wl = (uint32_t*)lds;
     uint32_t* const park = wl + lane;
     Entry* const stk = reinterpret_cast<Entry*>(wl + PK_WORDS4 * 64) + lane;
+    uint32_t* const coop = PHILOX ? wl + P.lds_wave_words - CO_WORDS : nullptr;
     const __amdgpu_buffer_rsrc_t nrsrc =
         NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
                           : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
@@ -1707,7 +1856,8 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
             v3_unpark(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib,
+                                    coop) == SHADE_ENDED;
             if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
@@ -2415,7 +2565,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // inside 10 × 512 B of LDS)
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
                                   ? (size_t)(persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
-                                        (size_t)(S.depth + 2) * 64 * (wide ? 4 : 2) + (size_t)g_lds_pad
+                                        (size_t)(S.depth + 2) * 64 * (wide ? 4 : 2) + (size_t)g_lds_pad +
+                                        (philox ? (size_t)dev::CO_WORDS * 4 : 0)
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
     size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes;

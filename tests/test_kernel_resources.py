@@ -33,7 +33,7 @@ def _v4(t, p, wd=0):
 HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + [_v4(t, p) for t in (0, 1) for p in (0, 1)] + \
       [_v3(t, p, 1, 1) for t in (0, 1) for p in (0, 1)] + [_v4(t, p, 1) for t in (0, 1) for p in (0, 1)]
 # register-held builds: a few bytes of cold spills (measured faster than the compiler's register count)
-SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 16}
+SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 24}
 
 
 def kernel_metadata(tmp_path):
