@@ -1,0 +1,2584 @@
+// render.hip — the MI355X (gfx950) per-pixel path-trace kernel and its launchers.
+//
+// Replaces __global__ Kernel / RenderInit / RandInit and the extern "C" launchers of
+// CudaRayTracer/src/Cuda/Kernel.cu:102-204.  Design:
+//   * one lane per pixel; a 256-thread workgroup renders a 16×16 pixel tile, each wave64 an 8×8 sub-tile
+//     so the primary rays of a wave are coherent;
+//   * the sample loop (Kernel.cu:137) and the bounce loop of color() (Kernel.cu:39) are flattened into
+//     ONE per-lane ray loop: a lane whose path ends starts its next sample at once instead of idling until
+//     the slowest lane of the wave finishes its path.  The per-lane order of RNG draws, and so the result,
+//     is unchanged;
+//   * closest hit through a binary BVH whose child boxes sit in the parent node (one 64-B node fetch
+//     tests two boxes), near-child-first traversal with a short per-lane stack; the scene tables are
+//     read through the L1/L2 or staged in LDS (template choice);
+//   * the cuRAND XORWOW state (Kernel.cu:123, 149) lives in VGPRs for the whole frame: 24 B loaded and
+//     24 B stored per pixel;
+//   * no MFMA: there is no dense contraction on this path.
+//
+// Arithmetic contract (bit-for-bit with oracle/rt_oracle.c): this file is compiled with
+// -ffp-contract=off; every +,-,*,/ and sqrtf of the reference expressions is one correctly rounded
+// binary32 operation, in the reference's association order.  Only the slab test of the BVH boxes uses
+// explicit FMAs: boxes are padded outward on the host, so box culling never rejects a primitive the
+// exact test accepts and the closest hit is decided by the exact primitive tests alone.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdio>
+#include <cstring>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <type_traits>
+
+#include "rt_internal.h"
+#include "rt_scene_device.h"
+
+namespace rt {
+namespace dev {
+
+// ---------------------------------------------------------------------------------------------------
+// Vec3 algebra (Utils/Math.cuh:16-229), one IEEE op per component, reference association order.
+// ---------------------------------------------------------------------------------------------------
+struct f3 {
+    float x, y, z;
+};
+
+// BVH node layouts read by the v3/v4 traversal (template argument NODES): 48 B of child boxes + a
+// separate table of packed 16-bit child references, or the 64-B node with both (rt_internal.h)
+enum NodeLayout { NODES_48 = 0, NODES_64 = 2 };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 scale(float t, f3 v) { return mk(t * v.x, t * v.y, t * v.z); }
+__device__ __forceinline__ f3 divs(f3 v, float t) { return mk(v.x / t, v.y / t, v.z / t); }
+__device__ __forceinline__ f3 neg(f3 v) { return mk(-v.x, -v.y, -v.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// sqrtf(x) for x >= 2^-96 (finite or +inf): the instruction sequence LLVM emits for the correctly rounded
+// square root — v_sqrt_f32 and a residual check of its two neighbours — without the small-input scaling
+// and the 0/inf class test, neither of which changes the result in that range (saves ~24 of ~54 cycles).
+__device__ __forceinline__ float sqrt_rn(const float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+    r = __builtin_fmaf(-sup, s, x) > 0.0f ? sup : r;
+    return r;
+}
+// sqrtf(x) bit for bit: sqrt_rn in its range, LLVM's full sequence (a branch no lane usually takes) below it
+__device__ __forceinline__ float sqrt_fast(const float x) { return x >= 0x1p-96f ? sqrt_rn(x) : sqrtf(x); }
+// RN(1/a) for |a| in [2^-40, 2^40]: v_rcp_f32 and one FMA Newton step — equal to the IEEE division for every
+// binary32 in that range, both signs (tools/check_rcp.hip, exhaustive on MI355X) — 12 issue cycles instead of
+// the ~36-cycle division sequence.  rcp_ieee keeps the IEEE division outside the range (a branch no lane
+// usually takes).
+__device__ __forceinline__ bool in_rcp_range(const float a) {
+    const float m = fabsf(a);
+    return m >= 0x1p-40f && m <= 0x1p40f;
+}
+__device__ __forceinline__ float rcp_rn(const float a) {
+    const float y = __builtin_amdgcn_rcpf(a);
+    return __builtin_fmaf(__builtin_fmaf(-a, y, 1.0f), y, y);
+}
+__device__ __forceinline__ float rcp_ieee(const float a) {
+    float r;
+    if (in_rcp_range(a)) r = rcp_rn(a);
+    else r = 1.0f / a;
+    return r;
+}
+__device__ __forceinline__ float length(f3 v) { return sqrt_fast(v.x * v.x + v.y * v.y + v.z * v.z); }
+__device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, length(v)); }
+__device__ __forceinline__ f3 normalize(f3 v) {
+    float inv = rcp_ieee(sqrt_fast(dot(v, v)));
+    return scale(inv, v);
+}
+// x / a correctly rounded from y = RN(1/a) (a one-off IEEE division) in five 2-cycle ops instead of the
+// ~36-cycle div_scale/rcp/div_fmas/div_fixup sequence: two residual corrections, the last of which is
+// exact by Markstein's theorem once its input is within an ulp.  Valid for |a| in [2^-40, 2^40] and
+// |x| >= 2^-100 or x == +0 (tools/check_fastdiv.c checks 1e10 random and near-tie cases bit for bit).
+__device__ __forceinline__ float div_rn(const float x, const float a, const float y) {
+    const float q0 = x * y;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-a, q0, x), y, q0);
+    return __builtin_fmaf(__builtin_fmaf(-a, q1, x), y, q1);
+}
+// divs(v, s) bit for bit, from y = RN(1/s) with |s| in [2^-40, 2^40] (y = 0 selects the IEEE division):
+// the fast path needs every |v_i / s| >= 2^-50 (so |v_i| >= 2^-90), anything else divides the IEEE way.
+__device__ __forceinline__ f3 divs_rn(const f3 v, const float s, const float y) {
+    const f3 q0 = mk(v.x * y, v.y * y, v.z * y);
+    if (fminf(fminf(fabsf(q0.x), fabsf(q0.y)), fabsf(q0.z)) >= 0x1p-50f) {
+        const float qx = __builtin_fmaf(__builtin_fmaf(-s, q0.x, v.x), y, q0.x);
+        const float qy = __builtin_fmaf(__builtin_fmaf(-s, q0.y, v.y), y, q0.y);
+        const float qz = __builtin_fmaf(__builtin_fmaf(-s, q0.z, v.z), y, q0.z);
+        return mk(__builtin_fmaf(__builtin_fmaf(-s, qx, v.x), y, qx), __builtin_fmaf(__builtin_fmaf(-s, qy, v.y), y, qy),
+                  __builtin_fmaf(__builtin_fmaf(-s, qz, v.z), y, qz));
+    }
+    return divs(v, s);
+}
+__device__ __forceinline__ float recip_in_range(const float s) {
+    return in_rcp_range(s) ? rcp_rn(s) : 0.0f;
+}
+__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }
+__device__ __forceinline__ float clampf(float x, float a, float b) { return (x < a) ? a : ((x > b) ? b : x); }
+__device__ __forceinline__ f3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
+
+// ---------------------------------------------------------------------------------------------------
+// cuRAND XORWOW (curand_kernel.h: curand(), _curand_uniform) in registers.
+// ---------------------------------------------------------------------------------------------------
+struct Rng {
+    uint32_t d, v0, v1, v2, v3, v4;
+};
+__device__ __forceinline__ float uniform(Rng& s) {
+    uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1;
+    s.v1 = s.v2;
+    s.v2 = s.v3;
+    s.v3 = s.v4;
+    uint32_t t2;  // t << 1 as a full-rate add (v_lshlrev_b32 issues at half rate on gfx950)
+    asm("v_add_u32 %0, %1, %1" : "=v"(t2) : "v"(t));
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ t2);
+    s.d += 362437u;
+    uint32_t x = s.v4 + s.d;
+    // x·2^-32 + 2^-33 (_curand_uniform): the product is exact, so one fma rounds like the mul + add
+    return __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f / 2.0f);
+}
+
+// RandomInUnitSphere (Math.cuh:252-260) with Random() (Math.cuh:231-234).  rtl: the components of
+// Vec3(ξa, ξb, ξc) are filled right to left (z = first draw), as the survey's g++ build evaluated it.
+// Groups of consecutive draws (same values, same order as that many uniform() calls).  For the XORWOW
+// state these are plain sequences; the Philox engine overloads them so a group generates at most one new
+// block of four words (one generation site per group instead of one per draw).
+template <class R> __device__ __forceinline__ void draw2(R& s, float& a, float& b) {
+    a = uniform(s);
+    b = uniform(s);
+}
+template <class R> __device__ __forceinline__ void draw3(R& s, float& a, float& b, float& c) {
+    a = uniform(s);
+    b = uniform(s);
+    c = uniform(s);
+}
+
+// 2·ξ − 1 of each component with one fma: 2·ξ is exact, so it rounds like the reference's mul + sub.  The
+// fill order is two selects per attempt (a launch-uniform branch around the loop measured the same).
+template <class R>
+__device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
+    f3 p;
+    do {
+        float a, b, c;
+        draw3(s, a, b, c);
+        const f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
+        p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
+    } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
+    return p;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Kernel parameters (by value; everything launch-uniform precomputed on the host with the same
+// binary32 operations the reference performs per thread).
+// ---------------------------------------------------------------------------------------------------
+struct KParams {
+    const float4* nodes;
+    const float4* nodes48;   // v3: three box float4 per node
+    const uint32_t* refs;    // v3: child references per node: two 16-bit in one word, or (wide) two words
+    const float4* prims;
+    const float4* mats;
+    const int4* imgs;
+    const uint8_t* texels;
+    uint32_t* pos;
+    float4* radiance;
+    float4* accum;
+    uint32_t* state;  // XORWOW states: 12-word rt_curand_state per pixel, or (RT_FLAG_STATE_SOA) six planes
+    uint32_t state_stride;  // distance between a pixel's state words: 1 (rt_curand_state) or the plane size
+    unsigned long long* counters;
+    uint32_t num_nodes, num_prims;
+    uint32_t width, height, spp, max_depth, flags;
+    uint32_t band_rows, num_ranks, rank, local_rows;
+    uint32_t tiles_x;
+    uint32_t grid_w, grid_h;  // pixels rendered: x < grid_w, global row < grid_h
+    uint32_t rius_rtl;
+    float width_f, cx, cy;
+    float inv_width;  // RN(1.0f / width_f) for div_rn
+    float near_plane, far_plane;
+    float origin[3], up[3], right[3];
+    float fov_fwd[3];  // inputs.fov * forwardV           (Kernel.cu:142)
+    float k10_fwd[3];  // (1.0f / inputs.fov * 10.0f) * forwardV (Kernel.cu:143)
+    float bg0[3], bg1[3];
+    uint32_t regen_threshold;  // v2: lanes still tracing below which finished lanes are regenerated
+    uint32_t* work_counter;    // v4: the frame's kQueueCounters queue heads, queue_stride words apart (zeroed before
+                               // the launch), then the exhausted-heads word
+    uint32_t queue_stride;     // v4: words between queue heads (RT_TUNE_QUEUE_STRIDE; 32 = 128 B)
+    uint32_t work_chunk;       // v4: work indices a wave takes per atomic (RT_TUNE_QUEUE_CHUNK; a multiple of 64)
+    uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
+    uint32_t work_per_counter; // v4: indices per queue head (a multiple of work_chunk): head k owns [k·n, (k+1)·n)
+    uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
+    uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
+    unsigned long long* wave_trace;  // diagnostic: v3 per tile {start, end}; v4 per wave {start, queue drained,
+                                     // end, pixels} of s_memrealtime (100 MHz)
+    const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
+    uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
+    uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
+};
+
+constexpr int kStackMax = 64;
+constexpr int kBlock = 256;
+// v4 work queue: the frame's work indices are split into this many contiguous ranges, each with its own
+// head 128 B from the next — one shared head serialises every wave's atomic in one L2 channel (≈ 16 ns
+// each: 0.5 ms for the 32400 chunks of a 1080p frame, the whole C5 frame time)
+constexpr uint32_t kQueueCounters = 16;  // <= 32: one word marks the exhausted heads (1-1024 heads measured)
+static_assert(kQueueCounters >= 1 && kQueueCounters <= 32, "queue heads");
+constexpr uint32_t kQueueAllDone = kQueueCounters == 32 ? 0xffffffffu : (1u << kQueueCounters) - 1u;
+
+// Traversal stack of each kernel family: per-lane scratch array (v1, any scene), 32-bit LDS entries
+// (v2, 32-bit references), 16-bit LDS entries (v3/v4, scenes whose references fit 16 bits)
+enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_LDS16 = 3 };
+
+// Per-lane traversal stack of the v1 kernel (the fallback for scenes the LDS kernels cannot hold)
+struct ScratchStack {
+    int s[kStackMax];
+    int n;
+    __device__ __forceinline__ void init(uint32_t*) { n = 0; }
+    __device__ __forceinline__ void push(int v) { s[n++] = v; }
+    __device__ __forceinline__ int pop() { return s[--n]; }
+    __device__ __forceinline__ bool empty() const { return n == 0; }
+};
+
+struct Counts {
+    uint32_t rays, boxes, prims, primary;
+    uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
+    uint32_t wnode_uniform = 0, wleaf_uniform = 0;  // COUNT_TESTS (v3): ... of them with one node / primitive
+    uint64_t ctrav = 0, cshade = 0, ctotal = 0, cleaf = 0;  // COUNT_TESTS (v3): wave clock cycles per phase
+    // COUNT_TESTS (v3): idle lanes summed over node iterations: pixel done / ray finished, waiting for the
+    // regeneration threshold / holding a leaf while the wave still visits nodes
+    uint64_t idle_nt = 0, idle_fin = 0, idle_wait = 0;
+};
+
+// 1 on the lowest active lane of the wave, 0 elsewhere (diagnostic wave-iteration counts).
+__device__ __forceinline__ uint32_t wave_leader() {
+    return __lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1) ? 1u : 0u;
+}
+
+constexpr int kEmpty = (int)0x80000000;
+constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX, rec) (Kernel.cu:40)
+// Conservative box culling.  A slab distance (plane - o)·(1/d) computed as fma(plane, rcp(d), -o·rcp(d)), with
+// rcp within 1 ulp, differs from the exact one by at most ~3·2^-24 of itself plus ~2^-24·|plane·rcp(d)|.  The
+// second term is covered by the host's outward box padding (1e-5 of the plane coordinate, scene_build.cpp);
+// the first grows with the distance travelled, so the far side of every slab interval is widened by a
+// relative 2^-20 (≥ 2·(3·2^-24)): a box the exact ray meets is never culled, whatever the camera distance.
+// (Widening only adds box visits; the closest hit is decided by the exact primitive tests.)
+constexpr float kSlabSlack = 1.0f + 0x1p-20f;
+
+// Closest hit (BVHNode::Hit, Hittable.cuh:387-439, and the primitive tests of PerformHit :470-485).
+// Returns the primitive index (BVH order) or -1, and the hit distance in t_best.
+template <bool COUNT>
+__device__ __forceinline__ int trace(const float4* __restrict__ nodes, const float4* __restrict__ prims,
+                                     uint32_t num_nodes, f3 o, f3 d, float a_dd, float& t_best, Counts& cnt) {
+    t_best = FLT_MAX;
+    int hit = -1;
+    if (num_nodes == 0) return -1;
+    // Slab test in fma form, t = lo·invd − o·invd, on boxes padded outward on the host.  A direction
+    // component that is exactly 0 (e.g. a Lambertian bounce whose tiny offset vanished against a large
+    // hit coordinate, (p + n + q) − p) would give inf − inf; clamping 1/d to ±1e20 keeps the test
+    // conservative: the position error of the fma form (~ulp of the coordinates) stays far below the
+    // 1e-5-relative box padding.
+    const f3 invd = mk(fminf(fmaxf(1.0f / d.x, -1e20f), 1e20f), fminf(fmaxf(1.0f / d.y, -1e20f), 1e20f),
+                       fminf(fmaxf(1.0f / d.z, -1e20f), 1e20f));
+    const float oix = o.x * invd.x, oiy = o.y * invd.y, oiz = o.z * invd.z;
+    ScratchStack stack;
+    stack.init(nullptr);
+    int node = 0;
+    while (true) {
+        while (node >= 0) {
+            const float4 n0 = nodes[4 * node + 0];
+            const float4 n1 = nodes[4 * node + 1];
+            const float4 n2 = nodes[4 * node + 2];
+            const float4 n3 = nodes[4 * node + 3];
+            const float a0 = __builtin_fmaf(n0.x, invd.x, -oix), a1 = __builtin_fmaf(n0.y, invd.x, -oix);
+            const float a2 = __builtin_fmaf(n0.z, invd.y, -oiy), a3 = __builtin_fmaf(n0.w, invd.y, -oiy);
+            const float a4 = __builtin_fmaf(n2.x, invd.z, -oiz), a5 = __builtin_fmaf(n2.y, invd.z, -oiz);
+            const float b0 = __builtin_fmaf(n1.x, invd.x, -oix), b1 = __builtin_fmaf(n1.y, invd.x, -oix);
+            const float b2 = __builtin_fmaf(n1.z, invd.y, -oiy), b3 = __builtin_fmaf(n1.w, invd.y, -oiy);
+            const float b4 = __builtin_fmaf(n2.z, invd.z, -oiz), b5 = __builtin_fmaf(n2.w, invd.z, -oiz);
+            const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+            const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best)) * kSlabSlack;
+            const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+            const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best)) * kSlabSlack;
+            if (COUNT) {
+                cnt.boxes += 2;
+                cnt.wnode += wave_leader();
+            }
+            const bool h0 = c0min <= c0max;
+            const bool h1 = c1min <= c1max;
+            const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+            if (h0 && h1) {
+                const bool swap = c1min < c0min;
+                node = swap ? ch1 : ch0;
+                stack.push(swap ? ch0 : ch1);
+            } else if (h0 | h1) {
+                node = h0 ? ch0 : ch1;
+            } else {
+                node = stack.empty() ? kEmpty : stack.pop();
+            }
+        }
+        if (node == kEmpty) break;
+        // leaf: primitives [first, first + count)
+        const uint32_t leaf = ~(uint32_t)node;
+        const uint32_t first = leaf >> 2, count = (leaf & 3u) + 1u;
+        for (uint32_t i = first; i < first + count; i++) {
+            const float4 p0 = prims[2 * i + 0];
+            const float4 p1 = prims[2 * i + 1];
+            const uint32_t type = __float_as_uint(p1.w) & 15u;
+            if (COUNT) {
+                cnt.prims++;
+                cnt.wleaf += wave_leader();
+            }
+            if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                const f3 oc = sub(o, xyz(p0));
+                const float b = dot(oc, d);
+                const float c = dot(oc, oc) - p1.x;  // p1.x = radius · radius
+                const float disc = b * b - a_dd * c;
+                if (disc > 0) {
+                    const float sq = sqrtf(disc);
+                    float t = (-b - sq) / a_dd;
+                    if (t < t_best && t > kTmin) {
+                        t_best = t;
+                        hit = (int)i;
+                    } else {
+                        t = (-b + sq) / a_dd;
+                        if (t < t_best && t > kTmin) {
+                            t_best = t;
+                            hit = (int)i;
+                        }
+                    }
+                }
+            } else {  // XY/XZ/YZRect::Hit (Hittable.cuh:140-169, 196-225, 252-281)
+                const float ok = type == RT_XYRECT ? o.z : (type == RT_XZRECT ? o.y : o.x);
+                const float dk = type == RT_XYRECT ? d.z : (type == RT_XZRECT ? d.y : d.x);
+                const float t = (p0.x - ok) * rcp_ieee(dk);
+                if (!(t < kTmin || t > t_best)) {
+                    const float oa = type == RT_YZRECT ? o.y : o.x, da = type == RT_YZRECT ? d.y : d.x;
+                    const float ob = type == RT_XYRECT ? o.y : o.z, db = type == RT_XYRECT ? d.y : d.z;
+                    const float x = oa + t * da;
+                    const float y = ob + t * db;
+                    if (!(x < p0.y || x > p0.z || y < p0.w || y > p1.x)) {
+                        t_best = t;
+                        hit = (int)i;
+                    }
+                }
+            }
+        }
+        if (stack.empty()) break;
+        node = stack.pop();
+    }
+    return hit;
+}
+
+// acos / atan2 of GetSphereUV (Hittable.cuh:119-125) as fixed sequences of binary32 +, -, *, / and sqrt
+// (Cephes asinf/atanf polynomials, ~2 ulp), identical operation for operation in oracle/rt_oracle.c.  The
+// reference's CUDA acos/atan2 under -use_fast_math cannot be reproduced, and the device library's and
+// libm's acosf/atan2f disagree in the last bit now and then, which moves a lookup into an 8192-wide texture
+// by one texel.  The acos argument is clamped to [-1, 1] (a rounded normal can exceed 1 by an ulp).
+__device__ __forceinline__ float rt_asin_poly(const float x) {  // |x| <= 0.5
+    const float z = x * x;
+    const float p = (((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+                    1.6666752422e-1f;
+    return p * z * x + x;
+}
+__device__ __forceinline__ float rt_acosf(float x) {
+    x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+    if (x < -0.5f) return 0x1.921fb6p+1f - 2.0f * rt_asin_poly(sqrtf(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * rt_asin_poly(sqrtf(0.5f * (1.0f - x)));
+    return 0x1.921fb6p+0f - rt_asin_poly(x);
+}
+__device__ __forceinline__ float rt_atan_poly(const float x) {  // |x| <= tan(pi/8)
+    const float z = x * x;
+    return (((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x + x;
+}
+__device__ __forceinline__ float rt_atan01(const float t) {  // t in [0, 1]
+    if (t > 0.41421356f) return 0x1.921fb6p-1f + rt_atan_poly((t - 1.0f) / (t + 1.0f));
+    return rt_atan_poly(t);
+}
+__device__ __forceinline__ float rt_atan2f(const float y, const float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    float r;
+    if (ax == 0.0f && ay == 0.0f) r = 0.0f;
+    else if (ay <= ax) r = rt_atan01(ay / ax);
+    else r = 0x1.921fb6p+0f - rt_atan01(ax / ay);
+    if (__builtin_signbit(x)) r = 0x1.921fb6p+1f - r;  // IEEE atan2: x < 0 or -0
+    return __builtin_signbit(y) ? -r : r;
+}
+
+// Texture::value (Texture.cuh:42-45, 58-67, 83-105)
+__device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, const float4& m2, uint32_t tex_type,
+                                            float u, float v, f3 p, const int4* __restrict__ imgs,
+                                            const uint8_t* __restrict__ texels) {
+    if (tex_type == RT_CONSTANT) return xyz(m1);
+    if (tex_type == RT_CHECKER) {
+        const float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+        return sines < 0 ? xyz(m1) : xyz(m2);
+    }
+    if (tex_type == RT_IMAGE) {
+        const int img = __float_as_int(m0.w);
+        if (img < 0) return mk(0.0f, 1.0f, 1.0f);  // no image (Texture.cuh:83-84: data == nullptr → cyan)
+        const int4 im = imgs[img];  // (byte offset of the texels, width, height, bytes per texel)
+        if (im.x < 0) return mk(0.0f, 1.0f, 1.0f);  // data == nullptr
+        u = clampf(u, 0.0f, 1.0f);
+        v = 1.0f - clampf(v, 0.0f, 1.0f);
+        int i = (int)(u * (float)im.y);
+        int j = (int)(v * (float)im.z);
+        if (i >= im.y) i = im.y - 1;
+        if (j >= im.z) j = im.z - 1;
+        const float color_scale = 1.0f / 255.0f;
+        const size_t texel = (size_t)j * (size_t)im.y + (size_t)i;
+        uint32_t r, g, b;
+        if (im.w == 4) {  // RGBA8-padded layout: one dword gather per texel
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(texels + im.x + texel * 4);
+            r = w & 0xffu;
+            g = (w >> 8) & 0xffu;
+            b = (w >> 16) & 0xffu;
+        } else {  // the reference's RGB8 layout (Texture.cuh:76, 96-104): three byte gathers
+            const uint8_t* px = texels + im.x + texel * 3;
+            r = px[0];
+            g = px[1];
+            b = px[2];
+        }
+        return mk(color_scale * (float)r, color_scale * (float)g, color_scale * (float)b);
+    }
+    return mk(0.0f, 0.0f, 0.0f);
+}
+
+__device__ __forceinline__ uint32_t f2u8(float f) { return f != f ? 0u : (uint32_t)(int)f; }
+
+// RgbToInt (Kernel.cu:12-19)
+__device__ __forceinline__ uint32_t rgb_to_int(float r, float g, float b) {
+    r = clampf(r, 0.0f, 255.0f);
+    g = clampf(g, 0.0f, 255.0f);
+    b = clampf(b, 0.0f, 255.0f);
+    return (255u << 24) | (f2u8(b) << 16) | (f2u8(g) << 8) | f2u8(r);
+}
+
+__device__ __forceinline__ uint32_t global_row(const KParams& P, uint32_t local_row) {
+    const uint32_t band = local_row / P.band_rows, within = local_row - band * P.band_rows;
+    return (band * P.num_ranks + P.rank) * P.band_rows + within;
+}
+
+// Launch-uniform camera / background terms (kernel arguments, SGPR-resident).
+struct Camera {
+    f3 origin, up, right, fov_fwd, k10_fwd;
+    float xf, yf;  // (x - center.x()), (center.y() - y) of this lane's pixel (Kernel.cu:139-140)
+};
+
+// Camera ray of one sample (Kernel.cu:139-146): two uniforms, then the reference's plane construction.
+template <class PP, class R>
+__device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& ro, f3& rd) {
+    float xi1, xi2;
+    draw2(rng, xi1, xi2);
+    // (x - cx + ξ) / width: the dividend is +0 or at least 2^-33 in magnitude (ξ in (0, 1]), inside div_rn's range
+    const float u = div_rn(cam.xf + xi1, P->width_f, P->inv_width);
+    const float v = div_rn(cam.yf + xi2, P->width_f, P->inv_width);
+    const f3 dist = add(scale(u, cam.right), scale(v, cam.up));
+    const f3 start = add(add(scale(P->near_plane, dist), cam.origin), cam.fov_fwd);
+    const f3 second = add(add(scale(P->far_plane, dist), cam.k10_fwd), cam.origin);
+    ro = start;
+    rd = normalize(sub(second, start));
+}
+
+// One iteration of color()'s bounce loop after the closest-hit query (Kernel.cu:40-76): sky on a miss,
+// emission, or Scatter of the hit material.  Returns SHADE_ENDED when the path ended (contribution in
+// `contrib`, `emitted * cur_attenuation` or `cur_attenuation * sky`), SHADE_CONTINUE when it continues with
+// (ro, rd, att).
+enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1 };
+template <bool TEX = true, class PP, class R>
+__device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
+                                     f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
+    // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
+    // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
+    // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
+    // primitive — the material load need not wait for the primitive's
+    uint32_t mtype = 0xffu;  // 0xff: miss
+    if (hit >= 0) mtype = __float_as_uint(P->mats[3 * (hit_tag >> 4)].x) & 15u;
+    const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
+    if (hit < 0) {  // sky (Kernel.cu:41-44)
+        // rd.y / |rd|: below |rd.y| = 2^-100 the quotient's exact bits vanish in the + 1 (|q| < 2^-60)
+        const float len = length(rd);
+        float q;
+        if (in_rcp_range(len)) q = div_rn(rd.y, len, rcp_rn(len));
+        else q = rd.y / len;
+        const float tt = 0.5f * (q + 1.0f);
+        const f3 c = add(scale(1.0f - tt, mk(P->bg0[0], P->bg0[1], P->bg0[2])), scale(tt, mk(P->bg1[0], P->bg1[1], P->bg1[2])));
+        contrib = mulv(att, c);
+        return SHADE_ENDED;
+    }
+    const float4 p0 = prims[2 * hit + 0];
+    const float4 p1 = prims[2 * hit + 1];
+    const uint32_t type = hit_tag & 15u, mat = hit_tag >> 4;
+    const float4 m0 = P->mats[3 * mat + 0];
+    const uint32_t ttype = (__float_as_uint(m0.x) >> 4) & 15u;
+    f3 p, normal;
+    float hu = 0.0f, hv = 0.0f;
+    if (type == RT_SPHERE) {  // hit record of Sphere::Hit (Hittable.cuh:91-95)
+        p = add(ro, scale(t, rd));
+        normal = divs_rn(sub(p, xyz(p0)), p0.w, p1.y);  // p1.y = RN(1/radius) or 0 (scene_build.cpp)
+        if (TEX && ttype == RT_IMAGE && mtype != RT_DIELECTRIC) {  // GetSphereUV (Hittable.cuh:119-125)
+            const float theta = rt_acosf(-normal.y);
+            const float phi = rt_atan2f(-normal.z, normal.x) + 3.141592654f;
+            hu = phi / (2 * 3.141592654f);
+            hv = theta / 3.141592654f;
+        }
+    } else {  // hit record of *Rect::Hit (Hittable.cuh:155-166)
+        const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+        const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+        const float xx = oa + t * da;
+        const float yy = ob + t * db;
+        hu = (xx - p0.y) / (p0.z - p0.y);
+        hv = (yy - p0.w) / (p1.x - p0.w);
+        const f3 outward = type == RT_XYRECT ? mk(0.0f, 0.0f, 1.0f)
+                           : type == RT_XZRECT ? mk(0.0f, 1.0f, 0.0f)
+                                               : mk(1.0f, 0.0f, 0.0f);
+        const bool front = dot(rd, outward) < 0;  // SetFaceNormal (Hittable.cuh:23-27)
+        normal = front ? outward : neg(outward);
+        p = add(ro, scale(t, rd));
+    }
+    if (mtype == RT_DIFFUSELIGHT) {  // DiffuseLight::Emitted (Material.cuh:164-176)
+        const float4 m1 = P->mats[3 * mat + 1];
+        f3 tex = xyz(m1);
+        if (TEX && ttype != RT_CONSTANT) {
+            const float4 m2 = P->mats[3 * mat + 2];
+            tex = texture_value(m0, m1, m2, ttype, hu, hv, p, P->imgs, P->texels);
+        }
+        const f3 e = scale(m0.z, tex);
+        contrib = mulv(e, att);
+        return SHADE_ENDED;
+    }
+    float len = 1.0f, y_len = 0.0f;
+    f3 ud = mk(0.0f, 0.0f, 0.0f);
+    if (specular) {
+        len = length(rd);
+        y_len = recip_in_range(len);
+        ud = divs_rn(rd, len, y_len);
+    }
+    if (mtype == RT_DIELECTRIC) {  // Dielectric::Scatter (Material.cuh:106-136); attenuation (1,1,1)
+        // Evaluated in an order that keeps few values live: every quantity is the same binary32 value the
+        // reference computes (pure functions of rd, normal, ir), and only the chosen direction is formed.
+        // m1 = (1.0f / ir, r0²) precomputed on the host with the same operations (rt_internal.h).
+        const float ir = m0.y;
+        const float4 m1 = P->mats[3 * mat + 1];
+        const float dn = dot(rd, normal);
+        const bool exiting = dn > 0.0f;
+        const float cn = exiting ? dn : -dn;
+        float cosine;
+        if (y_len != 0.0f && fabsf(cn) >= 0x1p-100f) cosine = div_rn(cn, len, y_len);
+        else cosine = cn / len;
+        if (exiting) cosine = sqrtf(1.0f - ir * ir * (1 - cosine * cosine));
+        const float ni_over_nt = exiting ? ir : m1.x;
+        const f3 outward_normal = exiting ? neg(normal) : normal;
+        // Refract (Math.cuh:292-304): uv = UnitVector(v)
+        const float dt = dot(ud, outward_normal);
+        const float discriminant = 1.0f - ni_over_nt * ni_over_nt * (1 - dt * dt);
+        float reflect_prob = 1.0f;
+        if (discriminant > 0) {  // Reflectance (Material.cuh:139-145)
+            const float r0 = m1.y;
+            const float xs = 1.0f - cosine;
+            const float x2 = xs * xs;
+            reflect_prob = r0 + (1.0f - r0) * ((x2 * x2) * xs);
+        }
+        const bool refl = uniform(rng) < reflect_prob;
+        if (refl) {
+            rd = reflect(rd, normal);
+        } else if (discriminant > 0) {
+            rd = sub(scale(ni_over_nt, sub(ud, scale(dt, outward_normal))), scale(sqrtf(discriminant), outward_normal));
+        } else {
+            rd = mk(0.0f, 0.0f, 0.0f);  // uninitialised `refracted` in the reference (ξ = 1.0, TIR)
+        }
+        ro = p;
+        return SHADE_CONTINUE;
+    }
+    const f3 q = random_in_unit_sphere(rng, rtl);
+    const float4 m1 = P->mats[3 * mat + 1];
+    f3 attenuation;
+    bool ok = true;
+    if (mtype == RT_LAMBERTIAN) {  // Lambertian::Scatter (Material.cuh:43-62)
+        const f3 target = add(add(p, normal), q);
+        rd = sub(target, p);
+    } else {  // Metal::Scatter (Material.cuh:75-94)
+        const f3 reflected = reflect(ud, normal);
+        rd = add(reflected, scale(m0.y, q));
+        ok = dot(rd, normal) > 0;
+    }
+    if (!TEX || ttype == RT_CONSTANT) {
+        attenuation = xyz(m1);
+    } else {
+        const float4 m2 = P->mats[3 * mat + 2];
+        attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, P->imgs, P->texels);
+    }
+    ro = p;
+    if (ok) {
+        att = mulv(attenuation, att);
+        return SHADE_CONTINUE;
+    }
+    contrib = mulv(mk(0.0f, 0.0f, 0.0f), att);  // emitted * cur_attenuation
+    return SHADE_ENDED;
+}
+
+// Pixel epilogue (Kernel.cu:149-157): RNG state store, average, gamma 2, RGBA8 pack; optional outputs.
+__device__ __forceinline__ void store_rng(const KParams& P, uint32_t* st, const Rng& rng) {
+    if (!(P.flags & RT_FLAG_NO_STATE_WRITEBACK)) {
+        const uint32_t k = P.state_stride;
+        if (k == 1u) {  // the reference's 48-B curandState: d, v[5] are its first 24 bytes
+            *reinterpret_cast<uint4*>(st) = make_uint4(rng.d, rng.v0, rng.v1, rng.v2);
+            *reinterpret_cast<uint2*>(st + 4) = make_uint2(rng.v3, rng.v4);
+        } else {  // six planes: each word a coalesced 4-B access of the wave
+            st[0] = rng.d;
+            st[k] = rng.v0;
+            st[2 * k] = rng.v1;
+            st[3 * k] = rng.v2;
+            st[4 * k] = rng.v3;
+            st[5 * k] = rng.v4;
+        }
+    }
+}
+
+template <class R>
+__device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32_t* st, const R& rng, f3 col) {
+    store_rng(P, st, rng);
+    f3 c;
+    if (P.flags & RT_FLAG_ACCUMULATE) {
+        float4 a = P.accum[pix];
+        a.x = a.x + col.x;
+        a.y = a.y + col.y;
+        a.z = a.z + col.z;
+        a.w = a.w + (float)P.spp;
+        P.accum[pix] = a;
+        c = divs(mk(a.x, a.y, a.z), a.w);
+    } else {
+        c = divs(col, (float)P.spp);
+    }
+    if (P.radiance) P.radiance[pix] = make_float4(c.x, c.y, c.z, 1.0f);
+    if (P.pos) P.pos[pix] = rgb_to_int(255.0f * sqrtf(c.x), 255.0f * sqrtf(c.y), 255.0f * sqrtf(c.z));
+}
+
+template <bool COUNT_TESTS>
+__device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt) {
+    if (P.counters) {
+        atomicAdd(&P.counters[0], (unsigned long long)cnt.rays);
+        if (COUNT_TESTS) {
+            atomicAdd(&P.counters[1], (unsigned long long)cnt.boxes);
+            atomicAdd(&P.counters[2], (unsigned long long)cnt.prims);
+            atomicAdd(&P.counters[4], (unsigned long long)cnt.wnode);
+            atomicAdd(&P.counters[5], (unsigned long long)cnt.wleaf);
+            atomicAdd(&P.counters[6], (unsigned long long)cnt.wshade);
+            atomicAdd(&P.counters[11], (unsigned long long)cnt.wnode_uniform);
+            atomicAdd(&P.counters[12], (unsigned long long)cnt.wleaf_uniform);
+            atomicAdd(&P.counters[13], (unsigned long long)cnt.idle_nt);
+            atomicAdd(&P.counters[14], (unsigned long long)cnt.idle_fin);
+            atomicAdd(&P.counters[15], (unsigned long long)cnt.idle_wait);
+            if (cnt.ctotal && wave_leader()) {  // one lane per wave: the stamps are wave-uniform
+                atomicAdd(&P.counters[7], (unsigned long long)cnt.ctrav);
+                atomicAdd(&P.counters[8], (unsigned long long)cnt.cshade);
+                atomicAdd(&P.counters[9], (unsigned long long)cnt.ctotal);
+                atomicAdd(&P.counters[10], (unsigned long long)cnt.cleaf);
+            }
+        }
+        atomicAdd(&P.counters[3], (unsigned long long)cnt.primary);
+    }
+}
+
+template <bool COUNT_TESTS, class R>
+__device__ __forceinline__ void finish_pixel(const KParams& P, size_t pix, uint32_t* st, const R& rng, f3 col,
+                                             const Counts& cnt) {
+    write_pixel(P, pix, st, rng, col);
+    flush_counts<COUNT_TESTS>(P, cnt);
+}
+
+// Lane → pixel.  BLOCK = 256: a workgroup covers a 16×16 tile, each wave an 8×8 sub-tile (P.tiles_x =
+// ceil(W/16)); BLOCK = 64: one wave per workgroup covering an 8×8 tile (P.tiles_x = ceil(W/8)).  Returns
+// false for lanes outside the (local) image or outside the faithful floor-division grid (Kernel.cu:184).
+template <int BLOCK = kBlock>
+__device__ __forceinline__ bool lane_pixel(const KParams& P, uint32_t& x, uint32_t& g, size_t& pix,
+                                           uint32_t tile = blockIdx.x) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t bx = tile % P.tiles_x, by = tile / P.tiles_x;
+    uint32_t ly;
+    if constexpr (BLOCK == 64) {
+        x = bx * 8 + (lane & 7u);
+        ly = by * 8 + (lane >> 3);
+    } else {
+        x = bx * 16 + (wave & 1u) * 8 + (lane & 7u);
+        ly = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    }
+    if (x >= P.width || ly >= P.local_rows) return false;
+    g = global_row(P, ly);
+    if (x >= P.grid_w || g >= P.grid_h) return false;
+    pix = (size_t)ly * P.width + x;
+    return true;
+}
+
+template <class PP>
+__device__ __forceinline__ Camera lane_camera(PP P, uint32_t x, uint32_t g) {
+    Camera c;
+    c.origin = mk(P->origin[0], P->origin[1], P->origin[2]);
+    c.up = mk(P->up[0], P->up[1], P->up[2]);
+    c.right = mk(P->right[0], P->right[1], P->right[2]);
+    c.fov_fwd = mk(P->fov_fwd[0], P->fov_fwd[1], P->fov_fwd[2]);
+    c.k10_fwd = mk(P->k10_fwd[0], P->k10_fwd[1], P->k10_fwd[2]);
+    c.xf = (float)(int)x - P->cx;
+    c.yf = P->cy - (float)(int)g;
+    return c;
+}
+
+// The kernel-argument block as a constant-address-space pointer the compiler cannot see through: fields
+// read through it are re-loaded with s_load where they are used, instead of being held in registers
+// across the traversal loop (launch-uniform camera/shading constants otherwise overflow the SGPR budget
+// and get parked in VGPRs, costing occupancy).
+typedef __attribute__((address_space(4))) const KParams KParamsC;
+__device__ __forceinline__ KParamsC* kparams_reload() {
+    KParamsC* p = (KParamsC*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// The pixel's first state word; its words are P.state_stride apart (1: rt_curand_state; the plane size with
+// RT_FLAG_STATE_SOA, whose planes hold the pixels 8×8 tile by tile — tile t, row r, column c at t·64 + 8r + c
+// — so the wave that renders a tile reads and writes 256 contiguous bytes per plane).
+__device__ __forceinline__ uint32_t soa_index(uint32_t x, uint32_t ly, uint32_t width) {
+    return ((((ly >> 3) * ((width + 7u) >> 3)) + (x >> 3)) << 6) + ((ly & 7u) << 3) + (x & 7u);
+}
+__device__ __forceinline__ uint32_t* state_at(const KParams& P, size_t pix) {
+    if (P.state_stride == 1u) return P.state + pix * 12;
+    const uint32_t ly = (uint32_t)(pix / P.width), x = (uint32_t)(pix - (size_t)ly * P.width);  // once per pixel
+    return P.state + soa_index(x, ly, P.width);
+}
+__device__ __forceinline__ Rng load_rng(const uint32_t* st, uint32_t k) {
+    if (k == 1u) {
+        const uint4 s03 = *reinterpret_cast<const uint4*>(st);
+        const uint2 s45 = *reinterpret_cast<const uint2*>(st + 4);
+        return Rng{s03.x, s03.y, s03.z, s03.w, s45.x, s45.y};
+    }
+    return Rng{st[0], st[k], st[2 * k], st[3 * k], st[4 * k], st[5 * k]};
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Perf-mode RNG (RT_FLAG_RNG_PHILOX): hipRAND/rocRAND Philox4x32-10 (rocrand_philox4x32_10.h:270-303,
+// rocrand_uniform.h:65-68, 239-242).  The pixel's stream is rocrand_init(seed, subsequence = global pixel
+// index, offset = frame << 34): draw n of the frame is word n & 3 of philox10(ctr = {n >> 2, frame,
+// pixel, 0}, key = seed), generated four at a time.  Nothing per pixel lives in HBM: the lane holds the
+// draw index, the current block of four words and the pixel index (six words, as the XORWOW state);
+// key and frame are launch-uniform kernel arguments.
+// ---------------------------------------------------------------------------------------------------
+struct RngPhilox {
+    uint32_t n, r0, r1, r2, r3, pix;
+    uint32_t k0, k1, frame;  // launch-uniform key and frame, read once when the stream is (un)parked
+};
+
+// Block `blk` of the lane's stream: philox10(ctr = {blk, frame, pixel, 0}, key = seed) into s.r0..r3.
+__device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
+    uint32_t c0 = blk, c1 = s.frame, c2 = s.pix, c3 = 0u;
+    uint32_t k0 = s.k0, k1 = s.k1;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {  // single_round + bumpkey (rocrand_philox4x32_10.h:286-303)
+        const uint64_t m0 = (uint64_t)0xD2511F53u * c0;  // one v_mad_u64_u32 for lo and hi
+        const uint64_t m1 = (uint64_t)0xCD9E8D57u * c2;
+        c0 = (uint32_t)(m1 >> 32) ^ c1 ^ k0;
+        c1 = (uint32_t)m1;
+        c2 = (uint32_t)(m0 >> 32) ^ c3 ^ k1;
+        c3 = (uint32_t)m0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    s.r0 = c0;
+    s.r1 = c1;
+    s.r2 = c2;
+    s.r3 = c3;
+}
+
+__device__ __forceinline__ float philox_to_uniform(uint32_t x) {
+    return __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f);  // 2^-32 + x·2^-32 (exact product)
+}
+
+// Word j (0..3) of the current block.
+// (Two selects on the index bits: LLVM turned the equivalent compare chain into a private array with
+// a lane-varying index, i.e. scratch stores and loads on every draw.)
+__device__ __forceinline__ uint32_t philox_word(const RngPhilox& s, uint32_t j) {
+    const bool odd = (j & 1u) != 0u, high = (j & 2u) != 0u;
+    const uint32_t lo = odd ? s.r1 : s.r0, hi = odd ? s.r3 : s.r2;
+    return high ? hi : lo;
+}
+
+__device__ __forceinline__ float uniform(RngPhilox& s) {
+    if ((s.n & 3u) == 0u) philox_block(s, s.n >> 2);
+    const float u = philox_to_uniform(philox_word(s, s.n & 3u));
+    s.n++;
+    return u;
+}
+
+// k (2 or 3) consecutive draws with at most one block generation: the words left in the current block
+// (none when n is a multiple of 4) come first, then the next block.
+template <int K>
+__device__ __forceinline__ void philox_group(RngPhilox& s, uint32_t* out) {
+    const uint32_t j = s.n & 3u;
+    const uint32_t left = j == 0u ? 0u : 4u - j;  // unused words of the current block
+    uint32_t old[3];
+#pragma unroll
+    for (int i = 0; i < K; i++) old[i] = philox_word(s, (j + (uint32_t)i) & 3u);
+    if (left < (uint32_t)K) philox_block(s, (s.n + left) >> 2);
+#pragma unroll
+    for (int i = 0; i < K; i++) out[i] = (uint32_t)i < left ? old[i] : philox_word(s, (uint32_t)i - left);
+    s.n += (uint32_t)K;
+}
+__device__ __forceinline__ void draw2(RngPhilox& s, float& a, float& b) {
+    uint32_t w[2];
+    philox_group<2>(s, w);
+    a = philox_to_uniform(w[0]);
+    b = philox_to_uniform(w[1]);
+}
+__device__ __forceinline__ void draw3(RngPhilox& s, float& a, float& b, float& c) {
+    uint32_t w[3];
+    philox_group<3>(s, w);
+    a = philox_to_uniform(w[0]);
+    b = philox_to_uniform(w[1]);
+    c = philox_to_uniform(w[2]);
+}
+
+__device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPhilox&) {}  // stateless in HBM
+
+// Start of a pixel's frame: its XORWOW state from HBM, or its Philox stream at draw 0.
+template <class R> __device__ __forceinline__ R begin_rng(const uint32_t* st, uint32_t stride, uint32_t pixel);
+template <> __device__ __forceinline__ Rng begin_rng<Rng>(const uint32_t* st, uint32_t stride, uint32_t) {
+    return load_rng(st, stride);
+}
+template <> __device__ __forceinline__ RngPhilox begin_rng<RngPhilox>(const uint32_t*, uint32_t, uint32_t pixel) {
+    KParamsC* q = kparams_reload();
+    return RngPhilox{0u, 0u, 0u, 0u, 0u, pixel, q->rng_key_lo, q->rng_key_hi, q->rng_frame};
+}
+
+// v1: Kernel (Kernel.cu:102-158) + color() (Kernel.cu:30-80), flattened into one per-lane ray loop: every
+// iteration traces one ray per lane to completion (trace(), scratch stack, 32-bit references), then
+// shades it.  The fallback for scenes whose BVH is too large or deep for the LDS-stack kernels.
+template <bool COUNT_TESTS>
+__global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
+    const float4* nodes = P.nodes;
+    const float4* prims = P.prims;
+    uint32_t x, g;
+    size_t pix;
+    if (!lane_pixel(P, x, g, pix)) return;
+    uint32_t* st = state_at(P, pix);
+    Rng rng = load_rng(st, P.state_stride);
+    const Camera cam = lane_camera(&P, x, g);
+    const bool rtl = P.rius_rtl != 0;
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    uint32_t sample = 0, depth = 0;
+    bool need_camera = true;
+
+    if (P.spp > 0) {
+        while (true) {
+            if (need_camera) {
+                camera_ray(&P, cam, rng, ro, rd);
+                att = mk(1.0f, 1.0f, 1.0f);
+                depth = 0;
+                need_camera = false;
+                cnt.primary++;
+            }
+            f3 contrib;
+            bool done = true;
+            if (depth >= P.max_depth) {
+                contrib = mk(0.0f, 0.0f, 0.0f);  // exceeded recursion (Kernel.cu:79)
+            } else {
+                cnt.rays++;
+                const float a_dd = dot(rd, rd);
+                float t;
+                const int hit = trace<COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, cnt);
+                if (COUNT_TESTS) cnt.wshade += wave_leader();
+                done = shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+                if (!done) depth++;
+            }
+            if (done) {
+                col = add(col, contrib);
+                if (++sample == P.spp) break;
+                need_camera = true;
+            }
+        }
+    }
+    finish_pixel<COUNT_TESTS>(P, pix, st, rng, col, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v2: resumable traversal.  Each lane carries its traversal state (node, postponed leaf, LDS stack,
+// closest hit) across iterations of one loop, in the structure of Aila & Laine's persistent
+// "while-while" kernel with speculative traversal:
+//   * internal nodes are visited until every lane of the wave has found a leaf; a lane's first leaf is
+//     postponed and it keeps traversing, so leaf tests run with most lanes active;
+//   * when fewer than `regen_threshold` lanes are still tracing, the wave leaves the traversal loop and
+//     the lanes whose query finished shade their hit and start their next ray (bounce or next sample),
+//     instead of idling until the slowest ray of the wave is done (path regeneration).
+// Per lane the sequence of rays, RNG draws and arithmetic is exactly that of render_kernel.
+// ---------------------------------------------------------------------------------------------------
+constexpr int kSentinel = 0x7fffffff;  // traversal finished (internal node ids are < it, leaves < 0)
+enum LaneMode { MODE_TRAV = 0, MODE_SHADE = 1, MODE_DONE = 2 };
+
+template <bool COUNT_TESTS, int BLOCK = 64>
+__global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
+    extern __shared__ float4 lds[];
+    uint32_t* const stk = (uint32_t*)lds + threadIdx.x;  // [depth][BLOCK] per-lane stacks
+    const float4* __restrict__ nodes = P.nodes;
+    const float4* __restrict__ prims = P.prims;
+    uint32_t x, g;
+    size_t pix;
+    if (!lane_pixel<BLOCK>(P, x, g, pix)) return;
+    uint32_t* st = state_at(P, pix);
+    Rng rng = load_rng(st, P.state_stride);
+    const Camera cam = lane_camera(&P, x, g);
+    const bool rtl = P.rius_rtl != 0;
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    f3 att = mk(1.0f, 1.0f, 1.0f);
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    uint32_t sample = 0, depth = 0;
+    // traversal state of the current ray
+    int node = kSentinel, leaf = 0, hit = -1;
+    uint32_t sp = 0;
+    float t_best = FLT_MAX, a_dd = 0.0f;
+    f3 invd = ro, oi = ro;
+    int mode = MODE_DONE;
+
+    // Start the closest-hit query of (ro, rd) (BVHNode::Hit with t in (0.001, FLT_MAX), Kernel.cu:40).
+    auto start_trace = [&]() {
+        cnt.rays++;
+        a_dd = dot(rd, rd);
+        invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
+                  fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
+                  fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
+        oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
+        t_best = FLT_MAX;
+        hit = -1;
+        node = P.num_nodes ? 0 : kSentinel;
+        leaf = 0;
+        sp = 0;
+        mode = MODE_TRAV;
+    };
+    // A path ended with `contrib`: accumulate (Kernel.cu:147) and begin the next sample, or finish.
+    auto next_sample = [&](f3 contrib) {
+        col = add(col, contrib);
+        while (++sample < P.spp) {
+            camera_ray(&P, cam, rng, ro, rd);
+            att = mk(1.0f, 1.0f, 1.0f);
+            depth = 0;
+            cnt.primary++;
+            if (P.max_depth > 0) {
+                start_trace();
+                return;
+            }
+            col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+        }
+        mode = MODE_DONE;
+    };
+
+    if (P.spp > 0) {
+        sample = (uint32_t)-1;
+        next_sample(mk(0.0f, 0.0f, 0.0f));  // col += 0 leaves col = +0 bit-exactly
+    }
+    const uint32_t threshold = P.regen_threshold;
+
+    while (true) {
+        if (mode == MODE_TRAV) {
+            while (node != kSentinel || leaf < 0) {
+                // internal nodes until every lane here has a postponed leaf.  Branch-free visit: the two
+                // stack entries a visit may pop are read before the node data arrives, the far child is
+                // written unconditionally above the stack top (kept only when both children are hit).
+                while ((uint32_t)node < (uint32_t)kSentinel) {
+                    const int top1 = (int)stk[((sp > 0u ? sp : 1u) - 1u) * BLOCK];
+                    const int top2 = (int)stk[((sp > 1u ? sp : 2u) - 2u) * BLOCK];
+                    const float4 n0 = nodes[4 * node + 0];
+                    const float4 n1 = nodes[4 * node + 1];
+                    const float4 n2 = nodes[4 * node + 2];
+                    const float4 n3 = nodes[4 * node + 3];
+                    const float a0 = __builtin_fmaf(n0.x, invd.x, -oi.x), a1 = __builtin_fmaf(n0.y, invd.x, -oi.x);
+                    const float a2 = __builtin_fmaf(n0.z, invd.y, -oi.y), a3 = __builtin_fmaf(n0.w, invd.y, -oi.y);
+                    const float a4 = __builtin_fmaf(n2.x, invd.z, -oi.z), a5 = __builtin_fmaf(n2.y, invd.z, -oi.z);
+                    const float b0 = __builtin_fmaf(n1.x, invd.x, -oi.x), b1 = __builtin_fmaf(n1.y, invd.x, -oi.x);
+                    const float b2 = __builtin_fmaf(n1.z, invd.y, -oi.y), b3 = __builtin_fmaf(n1.w, invd.y, -oi.y);
+                    const float b4 = __builtin_fmaf(n2.z, invd.z, -oi.z), b5 = __builtin_fmaf(n2.w, invd.z, -oi.z);
+                    const float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), kTmin));
+                    const float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t_best)) * kSlabSlack;
+                    const float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), kTmin));
+                    const float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t_best)) * kSlabSlack;
+                    if (COUNT_TESTS) {
+                        cnt.boxes += 2;
+                        cnt.wnode += wave_leader();
+                    }
+                    const bool h0 = c0min <= c0max;
+                    const bool h1 = c1min <= c1max;
+                    const bool both = h0 && h1, none = !(h0 || h1);
+                    const bool swap = c1min < c0min;
+                    const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+                    const int nearc = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
+                    const int farc = swap ? ch0 : ch1;
+                    stk[sp * BLOCK] = (uint32_t)farc;
+                    int nxt = none ? (sp > 0u ? top1 : kSentinel) : nearc;
+                    uint32_t nsp = both ? sp + 1u : ((none && sp > 0u) ? sp - 1u : sp);
+                    // first leaf: postpone it and pop the next entry (the stack top after this visit)
+                    const bool postpone = nxt < 0 && leaf == 0;
+                    const int after_top = both ? farc : (none ? (sp > 1u ? top2 : kSentinel) : (sp > 0u ? top1 : kSentinel));
+                    leaf = postpone ? nxt : leaf;
+                    nxt = postpone ? after_top : nxt;
+                    nsp = (postpone && nsp > 0u) ? nsp - 1u : nsp;
+                    node = nxt;
+                    sp = nsp;
+                    if (__ballot(leaf == 0) == 0) break;
+                }
+                // postponed leaves
+                while (leaf < 0) {
+                    const uint32_t l = ~(uint32_t)leaf;
+                    const uint32_t first = l >> 2, count = (l & 3u) + 1u;
+                    for (uint32_t i = first; i < first + count; i++) {
+                        const float4 p0 = prims[2 * i + 0];
+                        const float4 p1 = prims[2 * i + 1];
+                        const uint32_t type = __float_as_uint(p1.w) & 15u;
+                        if (COUNT_TESTS) {
+                            cnt.prims++;
+                            cnt.wleaf += wave_leader();
+                        }
+                        if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                            const f3 oc = sub(ro, xyz(p0));
+                            const float b = dot(oc, rd);
+                            const float c = dot(oc, oc) - p1.x;
+                            const float disc = b * b - a_dd * c;
+                            if (disc > 0) {
+                                const float sq = sqrtf(disc);
+                                float t = (-b - sq) / a_dd;
+                                if (t < t_best && t > kTmin) {
+                                    t_best = t;
+                                    hit = (int)i;
+                                } else {
+                                    t = (-b + sq) / a_dd;
+                                    if (t < t_best && t > kTmin) {
+                                        t_best = t;
+                                        hit = (int)i;
+                                    }
+                                }
+                            }
+                        } else {  // *Rect::Hit
+                            const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
+                            const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
+                            const float t = (p0.x - ok) * rcp_ieee(dk);
+                            if (!(t < kTmin || t > t_best)) {
+                                const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+                                const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+                                const float xx = oa + t * da;
+                                const float yy = ob + t * db;
+                                if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
+                                    t_best = t;
+                                    hit = (int)i;
+                                }
+                            }
+                        }
+                    }
+                    leaf = 0;
+                    if (node < 0) {  // another leaf was postponed in `node`: process it as well
+                        leaf = node;
+                        node = sp ? (int)stk[(--sp) * BLOCK] : kSentinel;
+                    }
+                }
+                if ((uint32_t)__popcll(__ballot(1)) < threshold) break;  // regenerate finished lanes
+            }
+            if (node == kSentinel && leaf == 0) mode = MODE_SHADE;
+        }
+        if (mode == MODE_SHADE) {
+            f3 contrib;
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            if (shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED) {
+                next_sample(contrib);
+            } else if (++depth >= P.max_depth) {
+                next_sample(mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+            } else {
+                start_trace();
+            }
+        }
+        if (__ballot(mode != MODE_DONE) == 0) break;
+    }
+    finish_pixel<COUNT_TESTS>(P, pix, st, rng, col, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v3: v2's resumable traversal with the register footprint cut for occupancy.
+//   * one wave per workgroup (no intra-workgroup coupling of wave lifetimes);
+//   * per-lane path state that only shading needs (cuRAND state, colour sum, attenuation, sample and
+//     depth counters) is parked in LDS while the lane traverses, and the ray's reciprocal direction /
+//     |d|² are recomputed on entry to the traversal phase: only the ray, the traversal cursor and the
+//     closest hit stay in VGPRs across phases;
+//   * 16-bit traversal stack entries in LDS when node and leaf references fit a signed 16 bits (the scene
+//     has < 32767 nodes and < 8192 primitives), 32-bit ones otherwise (WIDE instantiations, RefW below);
+//   * the lane's ray count is parked with the path state; primary samples = spp per pixel.
+// LDS per wave: 15 × 256 B of parked state + (depth + 2) × 128 B of stack (2 sentinel pads).
+// ---------------------------------------------------------------------------------------------------
+constexpr uint32_t kStackBase = 2;  // v3 stack entries start above two sentinel pads
+// Reference width of the v3/v4 kernels: 16-bit child and stack references (scenes with < 32767 nodes and < 8192
+// primitives: every BASELINE config), or 32-bit ones (WIDE: any scene the reference viewer can grow, AddHittable
+// CudaLayer.cpp:918-1370; 4-B LDS stack entries; the references' upper halves ride in the low bytes of the y
+// planes, scene_build.cpp).  References are unsigned in the width: internal nodes < kSentinel, leaves >= kLeaf.
+template <bool WIDE> struct RefW {
+    static constexpr uint32_t kSentinel = WIDE ? 0x7fffffffu : 0x7fffu;  // traversal finished
+    static constexpr uint32_t kLeaf = WIDE ? 0x80000000u : 0x8000u;      // references >= kLeaf are leaves
+    static constexpr uint32_t kMask = WIDE ? 0xffffffffu : 0xffffu;      // leaf ^ kMask = the leaf's ~ref
+    static constexpr uint32_t kLevelShift = WIDE ? 8u : 7u;              // log2(LDS bytes per stack level)
+    using Entry = typename std::conditional<WIDE, uint32_t, uint16_t>::type;
+};
+enum ParkSlot { PK_RNG = 0, PK_COL = 6, PK_ATT = 9, PK_SAMPLE = 12, PK_DEPTH = 13, PK_RAYS = 14, PK_WORDS = 15 };
+// Compact parking (v3, COMPACT): sample (13 bits), depth (6 bits) and the lane's ray count (13 bits) share
+// word PK_SD, so a wave parks 13 words instead of 15 — less LDS per wave, more resident waves (the v3
+// kernels are LDS-limited).  Valid when spp < 8192, max_depth < 64 and spp · max_depth < 8192.
+enum ParkSlotCompact { PK_SD = 12, PK_WORDS_COMPACT = 13 };
+__host__ __device__ constexpr int park_words(bool compact) { return compact ? PK_WORDS_COMPACT : PK_WORDS; }
+
+// Traversal cursor of one lane (v3).
+struct Cursor {
+    int node, leaf, hit;
+    uint32_t tag;  // type | material << 4 of the closest primitive so far
+    uint32_t sp;
+    float t_best;
+    int mode;
+};
+
+template <bool WIDE>
+__device__ __forceinline__ void v3_start_trace(uint32_t num_nodes, Cursor& c, uint32_t& rays) {
+    rays++;
+    c.t_best = FLT_MAX;
+    c.hit = -1;
+    c.node = num_nodes ? 0 : (int)RefW<WIDE>::kSentinel;
+    c.leaf = 0;
+    c.sp = kStackBase;
+    c.mode = MODE_TRAV;
+}
+
+// A path ended with `contrib`: accumulate (Kernel.cu:147), then the next sample's camera ray, or finish.
+template <bool WIDE, class R>
+__device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uint32_t g, f3 contrib, R& rng,
+                                               f3& col, f3& att, uint32_t& sample, uint32_t& depth, f3& ro,
+                                               f3& rd, Cursor& c, uint32_t& rays) {
+    col = add(col, contrib);
+    KParamsC* q = kparams_reload();
+    const Camera cam = lane_camera(q, x, g);
+    while (++sample < P.spp) {
+        camera_ray(q, cam, rng, ro, rd);
+        att = mk(1.0f, 1.0f, 1.0f);
+        depth = 0;
+        if (P.max_depth > 0) {
+            v3_start_trace<WIDE>(P.num_nodes, c, rays);
+            return;
+        }
+        col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+    }
+    c.mode = MODE_DONE;
+}
+
+// The six RNG words of a lane: XORWOW d, v[5]; Philox draw index, block of four words, pixel index.
+__device__ __forceinline__ void park_rng(uint32_t* park, const Rng& r) {
+    park[(PK_RNG + 0) * 64] = r.d;
+    park[(PK_RNG + 1) * 64] = r.v0;
+    park[(PK_RNG + 2) * 64] = r.v1;
+    park[(PK_RNG + 3) * 64] = r.v2;
+    park[(PK_RNG + 4) * 64] = r.v3;
+    park[(PK_RNG + 5) * 64] = r.v4;
+}
+__device__ __forceinline__ void park_rng(uint32_t* park, const RngPhilox& r) {
+    park[(PK_RNG + 0) * 64] = r.n;
+    park[(PK_RNG + 1) * 64] = r.r0;
+    park[(PK_RNG + 2) * 64] = r.r1;
+    park[(PK_RNG + 3) * 64] = r.r2;
+    park[(PK_RNG + 4) * 64] = r.r3;
+    park[(PK_RNG + 5) * 64] = r.pix;
+}
+__device__ __forceinline__ void unpark_rng(const uint32_t* park, Rng& r) {
+    r = Rng{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
+            park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64]};
+}
+__device__ __forceinline__ void unpark_rng(const uint32_t* park, RngPhilox& r) {
+    KParamsC* q = kparams_reload();
+    r = RngPhilox{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
+                  park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64],
+                  q->rng_key_lo, q->rng_key_hi, q->rng_frame};
+}
+
+template <bool COMPACT = false, class R>
+__device__ __forceinline__ void v3_park(uint32_t* park, const R& rng, f3 col, f3 att, uint32_t sample,
+                                        uint32_t depth, uint32_t rays) {
+    if constexpr (COMPACT) park[PK_SD * 64] = sample | (depth << 13) | (rays << 19);
+    else park[PK_RAYS * 64] = rays;
+    park_rng(park, rng);
+    park[(PK_COL + 0) * 64] = __float_as_uint(col.x);
+    park[(PK_COL + 1) * 64] = __float_as_uint(col.y);
+    park[(PK_COL + 2) * 64] = __float_as_uint(col.z);
+    park[(PK_ATT + 0) * 64] = __float_as_uint(att.x);
+    park[(PK_ATT + 1) * 64] = __float_as_uint(att.y);
+    park[(PK_ATT + 2) * 64] = __float_as_uint(att.z);
+    if constexpr (!COMPACT) {
+        park[PK_SAMPLE * 64] = sample;
+        park[PK_DEPTH * 64] = depth;
+    }
+}
+
+template <bool COMPACT = false, class R>
+__device__ __forceinline__ void v3_unpark(const uint32_t* park, R& rng, f3& col, f3& att, uint32_t& sample,
+                                          uint32_t& depth, uint32_t& rays) {
+    if constexpr (COMPACT) {
+        const uint32_t sd = park[PK_SD * 64];
+        sample = sd & 0x1fffu;
+        depth = (sd >> 13) & 0x3fu;
+        rays = sd >> 19;
+    } else {
+        rays = park[PK_RAYS * 64];
+    }
+    unpark_rng(park, rng);
+    col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
+             __uint_as_float(park[(PK_COL + 2) * 64]));
+    att = mk(__uint_as_float(park[(PK_ATT + 0) * 64]), __uint_as_float(park[(PK_ATT + 1) * 64]),
+             __uint_as_float(park[(PK_ATT + 2) * 64]));
+    if constexpr (!COMPACT) {
+        sample = park[PK_SAMPLE * 64];
+        depth = park[PK_DEPTH * 64];
+    }
+}
+
+
+// Constant-address-space views of the read-only scene buffers: loads from them at wave-uniform indices become
+// scalar loads (s_load_dword*) whose results feed VALU instructions as SGPR operands.
+typedef const __attribute__((address_space(4))) float ConstF32;
+typedef const __attribute__((address_space(4))) uint32_t ConstU32;
+typedef const __attribute__((address_space(4))) uint8_t ConstU8;
+template <class T> using Lds = __attribute__((address_space(3))) T;
+// v_min/v_max(3)_f32 as plain instructions: the operands are finite FMA results or canonical values
+__device__ __forceinline__ float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "s"(a), "v"(b)); return r; }
+__device__ __forceinline__ float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+__device__ __forceinline__ float vmax3(float a, float b, float c) { float r; asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
+__device__ __forceinline__ float vmin3(float a, float b, float c) { float r; asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
+constexpr uint32_t kPrimStep = 32u;  // leaf cursor unit: bytes of one 32-B primitive record
+
+// Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
+// until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
+// still tracing (the wave then shades the finished lanes and regenerates them).
+template <bool COUNT_TESTS, int NODES, uint32_t STK_OFF, bool WIDE>
+__device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
+                                            const float4* __restrict__ nodes_tab, const uint32_t* __restrict__ refs,
+                                            const float4* __restrict__ prims, typename RefW<WIDE>::Entry* const stk,
+                                            const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
+                                            Counts& cnt, const uint32_t ntrav = 64) {
+    // node / leaf references as unsigned values of the reference width (RefW): internal nodes < kSentinel, leaf
+    // references (negative in the layout) >= kLeaf; leaf == 0: no postponed leaf
+    using RW = RefW<WIDE>;
+    using Entry = typename RW::Entry;
+    uint32_t node = (uint32_t)c.node, leaf = (uint32_t)c.leaf;
+    int hit = c.hit;
+    uint32_t tag = c.tag;
+    uint32_t sp = c.sp;
+    float t_best = c.t_best;
+    const float a_dd = dot(rd, rd);
+    // RN(1/a) for the sphere roots (div_rn); outside [2^-40, 2^40] the test divides the IEEE way
+    const bool fast_div = a_dd >= 0x1p-40f && a_dd <= 0x1p40f;
+    const float inv_a = rcp_rn(a_dd);  // used only when fast_div
+    const f3 invd = mk(fminf(fmaxf(__builtin_amdgcn_rcpf(rd.x), -1e20f), 1e20f),
+                       fminf(fmaxf(__builtin_amdgcn_rcpf(rd.y), -1e20f), 1e20f),
+                       fminf(fmaxf(__builtin_amdgcn_rcpf(rd.z), -1e20f), 1e20f));
+    const f3 oi = mk(ro.x * invd.x, ro.y * invd.y, ro.z * invd.z);
+    // (invd, 0) or (0, invd) by sign with one max / min each (invd is never NaN; a -0 that became +0
+    // changes only the sign of a zero plane distance, which no comparison sees)
+    const f3 pa = mk(fmaxf(invd.x, 0.0f), fmaxf(invd.y, 0.0f), fmaxf(invd.z, 0.0f));
+    const f3 pc = mk(fminf(invd.x, 0.0f), fminf(invd.y, 0.0f), fminf(invd.z, 0.0f));
+    const Entry* ustk = stk;
+    // LDS address of this lane's stack entry 0 split into the lane part (VGPR) and the stack region's offset
+    // STK_OFF (an immediate of the ds instructions)
+    const uint32_t stk_lane = (uint32_t)(uintptr_t)(Lds<Entry>*)stk - STK_OFF;  // LDS base + the lane's column
+    // structured (stride 48 B) view of the node boxes for the vector path's idxen loads
+    const __amdgpu_buffer_rsrc_t rsrc_nodes_idx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)nodes_tab, (short)48, 0x7fffffff, 0x00020000);
+    constexpr uint32_t stk_off = STK_OFF / sizeof(Entry);  // in entries
+    const float tmin_s = kTmin;  // an SGPR operand of the slab test's v_max
+    const __amdgpu_buffer_rsrc_t prsrc = __builtin_amdgcn_make_buffer_rsrc((void*)prims, (short)0, 0x7fffffff, 0x00020000);
+    while (node != RW::kSentinel || leaf >= RW::kLeaf) {
+        // t_best changes only in the leaf phase: canonicalised once here, not on every visit by fminf
+        const float t_best_c = __builtin_canonicalizef(t_best);
+        const uint32_t n_outer = COUNT_TESTS ? (uint32_t)__popcll(__ballot(1)) : 0u;  // lanes still tracing
+        (void)n_outer;
+        // lanes holding no leaf yet, carried through the visits as an SGPR mask
+        uint64_t lzm = __ballot(leaf == 0);
+        while (node < RW::kSentinel) {
+            // the entry address as one v_lshl_add_u32 (LLVM emits a half-rate shift plus an add: C2 −0.2 %,
+            // C3 −0.3 %, profiles/r02e_ab_stack_addr.txt)
+            uint32_t sa;
+            asm("v_lshl_add_u32 %0, %1, %3, %2" : "=v"(sa) : "v"(sp), "v"(stk_lane), "i"(RW::kLevelShift));
+            Lds<Entry>* const sp_entry = (Lds<Entry>*)(uintptr_t)sa + stk_off;
+            uint32_t top1 = sp_entry[-64];
+            uint32_t top2 = sp_entry[-128];
+            // materialise the zero-extended words here: used in another basic block, a loaded u16 would
+            // otherwise be re-extended there with a v_and per word and visit
+            asm("" : "+v"(top1));
+            asm("" : "+v"(top2));
+            float c0min, c0max, c1min, c1max;
+            uint32_t ch0, ch1;
+            // near/far plane distances without min/max (4-cycle ops on gfx950): with (pa, pc) = (1/d, 0) for a
+            // positive direction component and (0, 1/d) for a negative one,
+            //   near = fma(lo, pa, fma(hi, pc, -o/d)),  far = fma(hi, pa, fma(lo, pc, -o/d))
+            // is fma(lo or hi, 1/d, -o/d) with one rounding — the value min/max of the two would pick — at four
+            // 2-cycle FMAs per axis instead of two FMAs, a min and a max.
+            const auto slab = [&](const float4 n0, const float4 n1, const float4 n2) {
+                const float nx0 = __builtin_fmaf(n0.x, pa.x, __builtin_fmaf(n0.y, pc.x, -oi.x));
+                const float fx0 = __builtin_fmaf(n0.y, pa.x, __builtin_fmaf(n0.x, pc.x, -oi.x));
+                const float ny0 = __builtin_fmaf(n0.z, pa.y, __builtin_fmaf(n0.w, pc.y, -oi.y));
+                const float fy0 = __builtin_fmaf(n0.w, pa.y, __builtin_fmaf(n0.z, pc.y, -oi.y));
+                const float nz0 = __builtin_fmaf(n2.x, pa.z, __builtin_fmaf(n2.y, pc.z, -oi.z));
+                const float fz0 = __builtin_fmaf(n2.y, pa.z, __builtin_fmaf(n2.x, pc.z, -oi.z));
+                const float nx1 = __builtin_fmaf(n1.x, pa.x, __builtin_fmaf(n1.y, pc.x, -oi.x));
+                const float fx1 = __builtin_fmaf(n1.y, pa.x, __builtin_fmaf(n1.x, pc.x, -oi.x));
+                const float ny1 = __builtin_fmaf(n1.z, pa.y, __builtin_fmaf(n1.w, pc.y, -oi.y));
+                const float fy1 = __builtin_fmaf(n1.w, pa.y, __builtin_fmaf(n1.z, pc.y, -oi.y));
+                const float nz1 = __builtin_fmaf(n2.z, pa.z, __builtin_fmaf(n2.w, pc.z, -oi.z));
+                const float fz1 = __builtin_fmaf(n2.w, pa.z, __builtin_fmaf(n2.z, pc.z, -oi.z));
+                // the plane distances are FMA results and t_best_c is canonical, so min/max need no
+                // canonicalising v_max (LLVM re-emits one per visit for a value carried into the loop:
+                // C2 −1.8 %)
+                c0min = vmax3(nx0, ny0, vmax(tmin_s, nz0));
+                c0max = vmin3(fx0, fy0, vmin(fz0, t_best_c)) * kSlabSlack;
+                c1min = vmax3(nx1, ny1, vmax(tmin_s, nz1));
+                c1max = vmin3(fx1, fy1, vmin(fz1, t_best_c)) * kSlabSlack;
+            };
+            if constexpr (NODES == NODES_64) {  // 64-B node: f32 boxes + two int32 references
+                const uint32_t noff = (uint32_t)node << 6;
+                const uint2 r2 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(nrsrc, noff + 48u, 0, 0));
+                ch0 = r2.x & RW::kMask;
+                ch1 = r2.y & RW::kMask;
+                slab(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff, 0, 0)),
+                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 16u, 0, 0)),
+                     __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nrsrc, noff + 32u, 0, 0)));
+            } else {  // 48 B of f32 boxes + 4 B of references
+                const uint32_t nu = __builtin_amdgcn_readfirstlane(node);
+                if (__ballot(node != nu) == 0) {
+                    // every active lane visits the same node: scalar loads through the constant cache, planes as
+                    // SGPR operands of the FMAs — no vector-memory (TA/TD) traffic, the kernel's busiest unit
+                    const ConstF32* cn = (const ConstF32*)((const ConstU8*)nodes_tab + nu * 48u);
+                    if constexpr (WIDE) {
+                        const ConstU32* r = (const ConstU32*)((const ConstU8*)refs + nu * 8u);
+                        ch0 = r[0];
+                        ch1 = r[1];
+                    } else {
+                        const uint32_t r = *(const ConstU32*)((const ConstU8*)refs + nu * 4u);
+                        ch0 = r & 0xffffu;
+                        ch1 = r >> 16;
+                    }
+                    slab(make_float4(cn[0], cn[1], cn[2], cn[3]), make_float4(cn[4], cn[5], cn[6], cn[7]),
+                         make_float4(cn[8], cn[9], cn[10], cn[11]));
+                } else {
+                    // Three structured (idxen) buffer loads: the descriptor's 48-B stride scales the node index in
+                    // the addresser (no VALU offset arithmetic: C2 −0.5 %), and the child references ride in the low
+                    // bytes of the x planes (scene_build.cpp), so no fourth load (C2 −1.6 %: the texture addresser
+                    // limits this loop as much as the VALU does — a fifth load costs +6.6 %;
+                    // profiles/r02e_ab_idxen.txt, profiles/r02e_ab_node_loads.txt).  The builtins have no idxen form:
+                    // the loads and their wait are one asm block.
+                    float4 n0, n1, n2;
+                    asm volatile(
+                        "buffer_load_dwordx4 %0, %3, %4, 0 idxen\n\t"
+                        "buffer_load_dwordx4 %1, %3, %4, 0 idxen offset:16\n\t"
+                        "buffer_load_dwordx4 %2, %3, %4, 0 idxen offset:32\n\t"
+                        "s_waitcnt vmcnt(0)"
+                        : "=&v"(n0), "=&v"(n1), "=&v"(n2)
+                        : "v"(node), "s"(rsrc_nodes_idx));
+                    // byte 0 of lo_x | byte 0 of hi_x << 8 (v_perm: bytes 0-3 = src1, 4-7 = src0, 0x0c = zero)
+                    // (a VOP3 takes no literal on gfx9: the selector is an SGPR operand)
+                    asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch0) : "v"(n0.y), "v"(n0.x), "s"(0x0c0c0400u));
+                    asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch1) : "v"(n1.y), "v"(n1.x), "s"(0x0c0c0400u));
+                    if constexpr (WIDE) {  // bits 16-31: byte 0 of lo_y | byte 0 of hi_y << 8, then the two halves
+                        uint32_t u0, u1;
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(u0) : "v"(n0.w), "v"(n0.z), "s"(0x0c0c0400u));
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(u1) : "v"(n1.w), "v"(n1.z), "s"(0x0c0c0400u));
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch0) : "v"(u0), "v"(ch0), "s"(0x05040100u));
+                        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(ch1) : "v"(u1), "v"(ch1), "s"(0x05040100u));
+                    }
+                    slab(n0, n1, n2);
+                }
+            }
+            if (COUNT_TESTS) {
+                cnt.boxes += 2;
+                cnt.wnode += wave_leader();
+                if (__ballot(node != (uint32_t)__builtin_amdgcn_readfirstlane(node)) == 0) cnt.wnode_uniform += wave_leader();
+                const uint32_t act = (uint32_t)__popcll(__ballot(1));
+                if (wave_leader()) {
+                    cnt.idle_nt += 64u - ntrav;
+                    cnt.idle_fin += ntrav - n_outer;
+                    cnt.idle_wait += n_outer - act;
+                }
+            }
+            // The visit decision as one block of lane-mask arithmetic (C2 −0.7 % against its C++ statement,
+            // profiles/r02h_ab_asm_decide.txt): the hit / order / leaf masks stay in SGPR pairs (SALU combines
+            // them), the "no leaf held yet" mask is carried in SGPRs through the visits, and the exit test needs
+            // no VALU materialisation of a ballot.  In C++ terms, with h0/h1 = child hit, swap = c1min < c0min:
+            //   both = h0 && h1, none = !(h0 || h1); near = both ? (swap ? ch1 : ch0) : (h0 ? ch0 : ch1);
+            //   far = swap ? ch0 : ch1 is written at the stack top unconditionally (kept when both);
+            //   next = none ? top1 : near; sp += both - none (the sentinel pads make an empty pop yield the
+            //   sentinel); a first leaf (next >= 0x8000 with no leaf held) is postponed: leaf = next and
+            //   next = the new stack top (both ? far : none ? top2 : top1), sp -= 1.
+            {
+                uint32_t farc, xr, nxt, at;
+                uint64_t m0, m1, m2, m3, m4, m5;
+                asm volatile(
+                    "v_cmp_le_f32 %[m0], %[a0], %[b0]\n\t"            // h0
+                    "v_cmp_le_f32 %[m1], %[a1], %[b1]\n\t"            // h1
+                    "v_cmp_lt_f32 %[m2], %[a1], %[a0]\n\t"            // swap
+                    "v_cndmask_b32 %[farc], %[ch1], %[ch0], %[m2]\n\t" // far child = swap ? ch0 : ch1
+                    "s_orn2_b64 %[m2], %[m2], %[m0]\n\t"              // swap | !h0
+                    "s_and_b64 %[m2], %[m2], %[m1]\n\t"               // take ch1 first
+                    "v_cndmask_b32 %[xr], %[ch0], %[ch1], %[m2]\n\t"
+                    "s_and_b64 %[m2], %[m0], %[m1]\n\t"               // both
+                    "s_or_b64 %[m0], %[m0], %[m1]\n\t"                // any
+                    "v_cndmask_b32 %[nxt], %[t1], %[xr], %[m0]\n\t"    // next = any ? first : pop
+                    "v_cndmask_b32 %[at], %[t2], %[t1], %[m0]\n\t"     // the stack top after this visit
+                    "v_cndmask_b32 %[at], %[at], %[farc], %[m2]\n\t"
+                    "v_addc_co_u32 %[sp], %[m3], %[sp], 0, %[m2]\n\t"  // push
+                    "s_not_b64 %[m0], %[m0]\n\t"                      // none
+                    "v_subb_co_u32 %[sp], %[m3], %[sp], 0, %[m0]\n\t"  // pop
+                    "v_cmp_lt_u32 %[m1], %[sent], %[nxt]\n\t"         // next is a leaf
+                    "s_mov_b64 %[m4], %[lzm]\n\t"                     // no leaf held yet (carried mask)
+                    "s_and_b64 %[m1], %[m1], %[m4]\n\t"               // postpone
+                    "v_cndmask_b32 %[leaf], %[leaf], %[nxt], %[m1]\n\t"
+                    "v_cndmask_b32 %[node], %[nxt], %[at], %[m1]\n\t"
+                    "v_subb_co_u32 %[sp], %[m3], %[sp], 0, %[m1]\n\t"  // pop the entry under the postponed leaf
+                    "s_andn2_b64 %[m5], %[m4], %[m1]\n\t"             // lanes still without a leaf
+                    "s_mov_b64 %[lzm], %[m5]\n\t"
+                    "s_and_b64 %[m5], %[m5], exec"
+                    : [farc] "=&v"(farc), [xr] "=&v"(xr), [nxt] "=&v"(nxt), [at] "=&v"(at), [node] "=&v"(node),
+                      [sp] "+v"(sp), [leaf] "+v"(leaf), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
+                      [m3] "=&s"(m3), [m4] "=&s"(m4), [m5] "=&s"(m5), [lzm] "+s"(lzm)
+                    : [a0] "v"(c0min), [b0] "v"(c0max), [a1] "v"(c1min), [b1] "v"(c1max), [ch0] "v"(ch0),
+                      [ch1] "v"(ch1), [t1] "v"(top1), [t2] "v"(top2), [sent] "s"(RW::kSentinel));
+                (void)m0; (void)m2; (void)m3;
+                *sp_entry = (Entry)farc;
+                if (m5 == 0) break;
+            }
+        }
+        const uint64_t t_leaf = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        // One primitive per lane per iteration: a lane walks its leaf's primitives and then the leaves
+        // that follow on its stack with its own cursor, so lanes with short leaves do not wait for the
+        // wave's longest leaf (same primitives in the same order per lane as a per-leaf loop).
+        // cursor and end in units of kPrimStep (bytes of the 32-B primitive record with RT_PRIM_BUFFER)
+        uint32_t cur = 0u, end = 0u;
+        if (leaf >= RW::kLeaf) {
+            const uint32_t l = leaf ^ RW::kMask;
+            cur = (l >> 2) * kPrimStep;
+            end = cur + ((l & 3u) + 1u) * kPrimStep;
+        }
+        while (cur < end) {
+            {
+                const uint32_t i = cur / kPrimStep;  // the primitive's index (a shift, needed only on a hit)
+                // byte offsets through a buffer descriptor: no 64-bit address arithmetic per primitive, and
+                // two 16-B loads (two texture-addresser requests) per test
+                const float4 p0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, cur, 0, 0));
+                const float4 p1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, cur + 16u, 0, 0));
+                const uint32_t type = __float_as_uint(p1.w) & 15u;
+                if (COUNT_TESTS) {
+                    cnt.prims++;
+                    cnt.wleaf += wave_leader();
+                    if (__ballot(cur != (uint32_t)__builtin_amdgcn_readfirstlane(cur)) == 0) cnt.wleaf_uniform += wave_leader();
+                }
+                if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                    const f3 oc = sub(ro, xyz(p0));
+                    const float b = dot(oc, rd);
+                    const float c = dot(oc, oc) - p1.x;
+                    const float disc = b * b - a_dd * c;
+                    if (disc > 0) {
+                        const float sq = sqrt_fast(disc);
+                        float t = fast_div ? div_rn(-b - sq, a_dd, inv_a) : (-b - sq) / a_dd;
+                        if (t < t_best && t > kTmin) {
+                            t_best = t;
+                            hit = (int)i;
+                            tag = __float_as_uint(p1.w);
+                        } else {
+                            t = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
+                            if (t < t_best && t > kTmin) {
+                                t_best = t;
+                                hit = (int)i;
+                            tag = __float_as_uint(p1.w);
+                            }
+                        }
+                    }
+                } else {  // *Rect::Hit
+                    const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
+                    const float dk = type == RT_XYRECT ? rd.z : (type == RT_XZRECT ? rd.y : rd.x);
+                    const float t = (p0.x - ok) * rcp_ieee(dk);
+                    if (!(t < kTmin || t > t_best)) {
+                        const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
+                        const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
+                        const float xx = oa + t * da;
+                        const float yy = ob + t * db;
+                        if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
+                            t_best = t;
+                            hit = (int)i;
+                            tag = __float_as_uint(p1.w);
+                        }
+                    }
+                }
+            }
+            cur += kPrimStep;
+            if (cur == end) {
+                leaf = 0;
+                if (node >= RW::kLeaf) {
+                    leaf = node;
+                    const uint32_t l = leaf ^ RW::kMask;
+                    cur = (l >> 2) * kPrimStep;
+                    end = cur + ((l & 3u) + 1u) * kPrimStep;
+                    node = ustk[(sp - 1u) * 64];
+                    sp--;
+                }
+            }
+        }
+        if (COUNT_TESTS) cnt.cleaf += __builtin_amdgcn_s_memtime() - t_leaf;
+        if ((uint32_t)__popcll(__ballot(1)) < threshold) break;
+    }
+    c.node = (int)node;
+    c.leaf = (int)leaf;
+    c.hit = hit;
+    c.tag = tag;
+    c.sp = sp;
+    c.t_best = t_best;
+    if (node == RW::kSentinel && leaf == 0u) c.mode = MODE_SHADE;
+}
+
+// v3 kernel: one wave per workgroup, one 8×8 pixel tile per wave; LDS holds the wave's parked path state
+// and its traversal stacks (P.lds_wave_words words).
+template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false, bool COMPACT = false, bool WIDE = false>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KParams P) {
+    using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    using Entry = typename RefW<WIDE>::Entry;
+    constexpr int NODES = NODES_48;
+    extern __shared__ float4 lds[];
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t* const wl = (uint32_t*)lds;
+    uint32_t* const park = wl + lane;                                                  // word k: park[k * 64]
+    Entry* const stk = reinterpret_cast<Entry*>(wl + park_words(COMPACT) * 64) + lane;  // stk[j * 64]
+    // node boxes through a buffer descriptor: 32-bit offsets, no 64-bit address arithmetic per visit
+    const __amdgpu_buffer_rsrc_t nrsrc =
+        NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+                          : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+    const float4* __restrict__ prims = P.prims;
+    uint32_t x, g;
+    size_t pix;
+    const uint32_t slot = blockIdx.x;
+    const uint32_t tile = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
+    if (!lane_pixel<64>(P, x, g, pix, tile)) return;
+    const bool rtl = P.rius_rtl != 0;
+    stk[0] = (Entry)RefW<WIDE>::kSentinel;   // two sentinel pads below the stack: popping an empty stack
+    stk[64] = (Entry)RefW<WIDE>::kSentinel;  // yields the sentinel without a bounds test
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    Cursor c{(int)RefW<WIDE>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_DONE};
+
+    {  // first camera ray of the pixel
+        uint32_t* st = state_at(P, pix);
+        R rng = begin_rng<R>(st, P.state_stride, g * P.width + x);  // global pixel index (Kernel.cu:119)
+        f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
+        // (sample = -1: v3_next_sample starts sample 0; with spp = 0 it stays 0, so compact parking's packed
+        // sample field cannot spill into the ray count)
+        uint32_t sample = P.spp > 0 ? (uint32_t)-1 : 0u, depth = 0, rays = 0;
+        if (P.spp > 0) v3_next_sample<WIDE>(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
+        v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);  // (col + 0 = +0 above)
+    }
+    const uint32_t threshold = P.regen_threshold;
+
+    const uint64_t t_start = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+    const uint64_t w_start = __builtin_amdgcn_s_memtime();
+    while (true) {
+        const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
+        if (c.mode == MODE_TRAV) {
+            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt, ntrav);
+        }
+        const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
+        if (c.mode == MODE_SHADE) {
+            R rng;
+            f3 col, att;
+            uint32_t sample, depth, rays;
+            v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
+            f3 contrib;
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+                ended = true;
+                contrib = mk(0.0f, 0.0f, 0.0f);
+            }
+            if (ended) {
+                v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
+            } else {
+                v3_start_trace<WIDE>(P.num_nodes, c, rays);
+            }
+            v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);
+        }
+        if (COUNT_TESTS) cnt.cshade += __builtin_amdgcn_s_memtime() - t_b;
+        if (__ballot(c.mode != MODE_DONE) == 0) break;
+    }
+    if (COUNT_TESTS) cnt.ctotal = __builtin_amdgcn_s_memtime() - t_start;
+    if (P.wave_trace && wave_leader()) {
+        P.wave_trace[2 * tile] = rt_start;
+        P.wave_trace[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (P.tile_cost && wave_leader()) {  // this tile's cost for the next launch's longest-first order
+        const uint64_t c = (__builtin_amdgcn_s_memtime() - w_start) >> 8;
+        P.tile_cost[tile] = c > 0xffffffffull ? 0xffffffffu : (uint32_t)c;
+    }
+    R rng;
+    f3 col, att;
+    uint32_t sample, depth, rays;
+    v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
+    cnt.rays = rays;
+    cnt.primary = P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
+    finish_pixel<COUNT_TESTS>(P, pix, state_at(P, pix), rng, col, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v4: v3 made persistent, with per-lane pixel regeneration.
+//   v3 gives each lane one pixel for the wave's lifetime, so a lane whose 64 samples are done idles
+//   until the wave's slowest pixel finishes, and every wave pays a workgroup dispatch.  v4 launches
+//   only as many single-wave workgroups as fit on the device at once; the frame is a queue of work
+//   indices (8×8 tiles in row-major tile order, 64 indices per tile), and a lane that finishes its pixel
+//   takes the next index at once.  The wave pulls 64-index chunks from the frame's counter with one
+//   atomic per chunk; needy lanes take consecutive indices of the wave's chunk (ballot + mbcnt rank).
+//   Every pixel still runs the reference's per-pixel sample loop on its own cuRAND stream, so the
+//   result does not depend on which lane or wave renders it.  Every wave exits once the queue is empty
+//   and its lanes are done (no wave waits on another).
+// Requires spp ≥ 1 and max_depth ≥ 1 (rt_render uses v3 otherwise).
+// LDS per wave: 18 × 256 B of parked state + (depth + 2) × 128 B of stack.
+// ---------------------------------------------------------------------------------------------------
+enum ParkSlotV4 { PK_X = PK_WORDS, PK_G = PK_WORDS + 1, PK_PIX = PK_WORDS + 2, PK_WORDS4 = PK_WORDS + 3 };
+constexpr int MODE_NEED = 3;  // v4: lane waits for a pixel
+
+// Work index → pixel of the local image (8×8 tiles, row-major tile order); false when the index lies
+// outside the image or outside the rendered grid.
+__device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint32_t& x, uint32_t& g, uint32_t& pix) {
+    const uint32_t tile = idx >> 6, l = idx & 63u;
+    const uint32_t by = tile / P.tiles_x, bx = tile - by * P.tiles_x;
+    x = bx * 8u + (l & 7u);
+    const uint32_t ly = by * 8u + (l >> 3);
+    if (x >= P.width || ly >= P.local_rows) return false;
+    g = global_row(P, ly);
+    if (x >= P.grid_w || g >= P.grid_h) return false;
+    pix = ly * P.width + x;
+    return true;
+}
+
+template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false>
+__global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
+    using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    using Entry = typename RefW<WIDE>::Entry;
+    extern __shared__ float4 lds[];
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t* const wl = (uint32_t*)lds;
+    uint32_t* const park = wl + lane;
+    Entry* const stk = reinterpret_cast<Entry*>(wl + PK_WORDS4 * 64) + lane;
+    const __amdgpu_buffer_rsrc_t nrsrc =
+        NODES == NODES_64 ? __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes, (short)0, (int)(P.num_nodes * 64u), 0x00020000)
+                          : __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+    const float4* __restrict__ prims = P.prims;
+    const bool rtl = P.rius_rtl != 0;
+    stk[0] = (Entry)RefW<WIDE>::kSentinel;
+    stk[64] = (Entry)RefW<WIDE>::kSentinel;
+    park[PK_RAYS * 64] = 0u;
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    Cursor c{(int)RefW<WIDE>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_NEED};
+    uint32_t wq_next = 0u, wq_end = 0u;  // wave-uniform: the wave's current chunk of work indices
+    bool drained = false;                // wave-uniform: the frame's queue is empty
+    // wave-uniform: the queue head the wave draws from (one of kQueueCounters, each owning a contiguous
+    // range of the frame; a wave moves on to the next head when its own is exhausted) and heads tried
+    uint32_t qc = blockIdx.x % kQueueCounters, qtried = 0u;
+    uint32_t wave_pixels = 0u;           // wave-uniform: pixels this wave has taken
+    const uint32_t threshold = P.regen_threshold;
+    const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+    uint64_t rt_drained = 0u;
+
+    while (true) {
+        if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt);
+        R rng;
+        f3 col, att;
+        uint32_t sample, depth, rays;
+        bool cam = false, fin = false;
+        const bool shading = c.mode == MODE_SHADE;
+        if (shading) {
+            v3_unpark(park, rng, col, att, sample, depth, rays);
+            f3 contrib;
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+                ended = true;
+                contrib = mk(0.0f, 0.0f, 0.0f);
+            }
+            if (ended) {
+                col = add(col, contrib);  // Kernel.cu:147
+                if (++sample < P.spp) {
+                    cam = true;
+                } else {  // the pixel is done (Kernel.cu:149-157)
+                    const uint32_t pix = park[PK_PIX * 64];
+                    write_pixel(P, pix, state_at(P, pix), rng, col);
+                    fin = true;
+                }
+            } else {
+                v3_start_trace<WIDE>(P.num_nodes, c, rays);
+            }
+        }
+        // pixel regeneration: lanes without a pixel take the next work indices
+        bool need = fin || c.mode == MODE_NEED;
+        uint64_t needm = __ballot(need);
+        if (needm != 0) {
+            if (!shading && need) rays = park[PK_RAYS * 64];
+            while (needm != 0 && !drained) {
+                if (wq_next >= wq_end) {
+                    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+                    uint32_t base = 0u;
+                    if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, P.work_chunk);
+                    base = __builtin_amdgcn_readlane(base, leader);
+                    const uint32_t idx = qc * P.work_per_counter + base;
+                    if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
+                        // mark it in the exhausted-heads word and move to the next live head (so a wave
+                        // probes a few heads at the frame's end, not every one of them)
+                        uint32_t done = 0u;
+                        if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * P.queue_stride, 1u << qc);
+                        done = __builtin_amdgcn_readlane(done, leader) | (1u << qc);
+                        if (done == kQueueAllDone || ++qtried >= kQueueCounters) {
+                            drained = true;
+                            if (P.wave_trace) rt_drained = __builtin_amdgcn_s_memrealtime();
+                            break;
+                        }
+                        const uint32_t live = ~done & kQueueAllDone;        // (nonzero here)
+                        const uint32_t above = live & ~((2u << qc) - 1u);   // live heads after qc
+                        qc = (uint32_t)__builtin_ctz(above ? above : live);
+                        continue;
+                    }
+                    wq_next = idx;
+                    wq_end = idx + P.work_chunk;
+                }
+                const uint32_t avail = wq_end - wq_next;
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+                if (need && rank < avail) {
+                    uint32_t x, g, pix;
+                    if (work_pixel(P, wq_next + rank, x, g, pix)) {
+                        need = false;
+                        park[PK_X * 64] = x;
+                        park[PK_G * 64] = g;
+                        park[PK_PIX * 64] = pix;
+                        rng = begin_rng<R>(state_at(P, pix), P.state_stride, g * P.width + x);
+                        col = mk(0.0f, 0.0f, 0.0f);
+                        sample = 0u;
+                        cam = true;
+                    }
+                }
+                const uint32_t taken = min((uint32_t)__popcll(needm), avail);
+                wq_next += taken;
+                const uint64_t still = __ballot(need);
+                wave_pixels += (uint32_t)__popcll(needm & ~still);
+                needm = still;
+            }
+            if (need) c.mode = MODE_DONE;
+        }
+        if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
+            KParamsC* q = kparams_reload();
+            const Camera cam_l = lane_camera(q, park[PK_X * 64], park[PK_G * 64]);
+            camera_ray(q, cam_l, rng, ro, rd);
+            att = mk(1.0f, 1.0f, 1.0f);
+            depth = 0u;
+            v3_start_trace<WIDE>(P.num_nodes, c, rays);
+        }
+        if (shading || cam) v3_park(park, rng, col, att, sample, depth, rays);
+        if (__ballot(c.mode != MODE_DONE) == 0) break;
+    }
+    cnt.rays = park[PK_RAYS * 64];
+    // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
+    cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;
+    if (P.wave_trace && wave_leader()) {  // ramp / steady state / tail of the persistent grid (tools/v4_timeline.py)
+        unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
+        w[0] = rt_start;
+        w[1] = rt_drained;
+        w[2] = __builtin_amdgcn_s_memrealtime();
+        w[3] = wave_pixels;
+    }
+    flush_counts<COUNT_TESTS>(P, cnt);
+}
+
+// RenderInit (Kernel.cu:166-176): curand_init(seed_base + global_pixel_index, 0, 0).
+__device__ __forceinline__ void curand_init_state(unsigned long long seed, uint32_t* st, uint32_t k = 1u) {
+    const uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+    const uint32_t s1 = ((uint32_t)(seed >> 32)) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    if (k != 1u) {  // RT_FLAG_STATE_SOA: d, v[5] only, one plane each
+        st[0] = 6615241u + t1 + t0;
+        st[k] = 123456789u + t0;
+        st[2 * k] = 362436069u ^ t0;
+        st[3 * k] = 521288629u + t1;
+        st[4 * k] = 88675123u ^ t1;
+        st[5 * k] = 5783321u + t0;
+        return;
+    }
+    *reinterpret_cast<uint4*>(st) = make_uint4(6615241u + t1 + t0, 123456789u + t0, 362436069u ^ t0, 521288629u + t1);
+    *reinterpret_cast<uint4*>(st + 4) = make_uint4(88675123u ^ t1, 5783321u + t0, 0u, 0u);
+    *reinterpret_cast<uint4*>(st + 8) = make_uint4(0u, 0u, 0u, 0u);  // boxmuller_extra, pad, extra_double
+}
+
+__global__ __launch_bounds__(kBlock) void render_init_kernel(uint32_t* state, uint32_t width, uint32_t local_rows,
+                                                              uint32_t band_rows, uint32_t num_ranks, uint32_t rank,
+                                                              unsigned long long seed_base, uint32_t soa) {  // soa: plane size
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t n = (size_t)width * local_rows;
+    if (i >= n) return;
+    const uint32_t ly = (uint32_t)(i / width), x = (uint32_t)(i - (size_t)ly * width);
+    const uint32_t band = ly / band_rows, within = ly - band * band_rows;
+    const uint32_t g = (band * num_ranks + rank) * band_rows + within;
+    const uint32_t pixel_index = g * width + x;  // unsigned, as Kernel.cu:174
+    if (soa) curand_init_state(seed_base + pixel_index, state + soa_index(x, ly, width), soa);
+    else curand_init_state(seed_base + pixel_index, state + i * 12);
+}
+
+// LaunchRenderInit's kernel honours the caller's grid/block exactly (Kernel.cu:166-176).
+__global__ void render_init_grid_kernel(uint32_t* state, uint32_t width, uint32_t height) {
+    const uint32_t i = threadIdx.x + blockIdx.x * blockDim.x;
+    const uint32_t j = threadIdx.y + blockIdx.y * blockDim.y;
+    if (i >= width || j >= height) return;
+    const uint32_t pixel_index = j * width + i;
+    curand_init_state(1984ull + pixel_index, state + (size_t)pixel_index * 12);
+}
+
+// Longest-first launch order.  Wave lifetimes differ several-fold between tiles (glass and metal paths
+// run to depth 8, sky pixels end at once), and a frame's last waves otherwise run on a nearly empty GPU:
+// in a row-major launch the final quarter of a config-2 frame holds < 50 % of the steady-state waves.
+// After each launch this one-workgroup kernel buckets the tiles by the lifetime their wave just measured
+// (4 buckets per octave, most expensive first) into the order the next launch with the same tile grid
+// dispatches them in.  The order changes when waves start, never what they compute.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t c) {  // 0 = most expensive
+    if (c == 0u) return 127u;
+    const uint32_t msb = 31u - (uint32_t)__clz(c);
+    const uint32_t frac = msb >= 2u ? (c >> (msb - 2u)) & 3u : (c << (2u - msb)) & 3u;
+    return 127u - (msb * 4u + frac);
+}
+
+__global__ __launch_bounds__(1024) void plan_order_kernel(const uint32_t* __restrict__ cost,
+                                                          uint32_t* __restrict__ order, uint32_t n) {
+    __shared__ uint32_t start[128];
+    if (threadIdx.x < 128) start[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) atomicAdd(&start[cost_bucket(cost[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0u;
+        for (int b = 0; b < 128; b++) {
+            const uint32_t c = start[b];
+            start[b] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += 1024u) order[atomicAdd(&start[cost_bucket(cost[i])], 1u)] = i;
+}
+
+__global__ void rand_init_kernel(uint32_t* state) {  // RandInit (Kernel.cu:160-164)
+    if (threadIdx.x == 0 && blockIdx.x == 0) curand_init_state(1984ull, state);
+}
+
+}  // namespace dev
+
+// ---------------------------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+thread_local bool g_timing = false;
+thread_local float g_last_ms = -1.0f;
+thread_local float g_last_host_ms = -1.0f;  // LaunchKernel: host time of the scene-cache step
+thread_local int g_variant = -1;
+thread_local int g_last_variant = -1;  // the variant the last rt_render on this thread launched
+
+int hip_check(hipError_t e, const char* what, int code = RT_ERR_DEVICE) {
+    if (e == hipSuccess) return RT_OK;
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return code;
+}
+
+using KernelFn = void (*)(const dev::KParams);
+
+// The kernels librt_hip.so ships (rt_set_variant(i) selects kVariants[i]).  Round 1 measured 37 variants;
+// the ones that lost their A/B (LDS-staged scene tables, binary16 and 4-wide nodes, several waves per
+// workgroup, register-bound occupancy targets) were dropped (DESIGN.md §4 keeps their numbers).
+//   0  v1: scratch stack, 32-bit references       — fallback for scenes beyond 16-bit references and deep BVHs
+//   1  v2: 64-thread resumable, 32-bit LDS stacks — fallback for scenes beyond 16-bit references
+//   2  v3: 15-word parking                        — spp/depth too large for compact parking
+//   3  v3: 13-word compact parking                — automatic choice from 64 spp; below, timed against 4
+//   4  v4: persistent work queue, 64-B nodes      — timed against 3 below 64 spp (a compact-parking, 48-B-node,
+//         longest-first-ordered v4 measured slower on C2, C3 and C5: profiles/r02_ab_v3_v4compact_c2.txt,
+//         profiles/r02_configs_v345.txt)
+struct Variant {
+    int stack;        // StackKind
+    int lds_depth;    // v2: LDS stack entries per lane
+    int block;        // threads per workgroup
+    int kernel;       // 1, 2, 3, 4: v1..v4
+    bool compact;     // v3: 13-word parking (needs spp < 8192, max_depth < 64, spp · max_depth < 8192)
+};
+constexpr Variant kVariants[] = {
+    {dev::STACK_SCRATCH, 0, 256, 1, false}, {dev::STACK_LDS, 24, 64, 2, false}, {dev::STACK_LDS16, 0, 64, 3, false},
+    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false},
+};
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4;
+
+template <int W, bool PH = false, bool C = false, bool WD = false>
+KernelFn v3_pick(bool count, bool tex) {
+    if (tex) return count ? dev::render_kernel_v3<true, W, true, PH, C, WD> : dev::render_kernel_v3<false, W, true, PH, C, WD>;
+    return count ? dev::render_kernel_v3<true, W, false, PH, C, WD> : dev::render_kernel_v3<false, W, false, PH, C, WD>;
+}
+
+template <bool PH = false, bool WD = false>
+KernelFn v4_pick(bool count, bool tex) {
+    if (tex) return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH, WD> : dev::render_kernel_v4<false, true, dev::NODES_64, PH, WD>;
+    return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH, WD> : dev::render_kernel_v4<false, false, dev::NODES_64, PH, WD>;
+}
+
+constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
+constexpr int kPhiloxCompactWaves = 7;  // ... of the non-texture Philox build of variant 3
+
+KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
+    if (wide) {  // 32-bit references: builds of the compact v3 and of v4 only (rt_render maps wide scenes there)
+        if (variant == kVarV3Compact)
+            return philox ? v3_pick<1, true, true, true>(count, tex) : v3_pick<1, false, true, true>(count, tex);
+        return philox ? v4_pick<true, true>(count, tex) : v4_pick<false, true>(count, tex);
+    }
+    switch (variant) {
+    case kVarV1: return count ? dev::render_kernel<true> : dev::render_kernel<false>;
+    case kVarV2: return count ? dev::render_kernel_v2<true> : dev::render_kernel_v2<false>;
+    case kVarV3: return philox ? v3_pick<1, true>(count, tex) : v3_pick<1>(count, tex);
+    case kVarV3Compact:
+        // Waves per SIMD by registers (profiles/r02_ab_builds_c2.txt): XORWOW held to 64 VGPRs (8 waves,
+        // 28 B of cold spills) 16.98 vs 17.25 ms at the compiler's 68; Philox held to 72 (7 waves) 21.5 vs
+        // 21.9 ms at 75, while 8 waves (64 VGPRs, 40 B of spills) ran 22.6 ms
+        if (philox)
+            return tex ? v3_pick<1, true, true>(count, true) : v3_pick<kPhiloxCompactWaves, true, true>(count, false);
+        return tex ? v3_pick<1, false, true>(count, true) : v3_pick<kXorwowCompactWaves, false, true>(count, false);
+    default: return philox ? v4_pick<true>(count, tex) : v4_pick<false>(count, tex);
+    }
+}
+
+thread_local int g_regen_threshold = 40;
+thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupancy experiments)
+thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
+thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
+thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
+
+// Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
+// Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
+// evicts the cache meanwhile (the buffers are freed when the last holder drops it; hipFree waits for the
+// device, so a launch still reading them completes first).
+struct TilePlan {
+    uint32_t* cost = nullptr;
+    uint32_t* order = nullptr;
+    std::atomic<bool> valid{false};  // an order has been planned (by an earlier launch on the same stream)
+    ~TilePlan() {
+        if (cost) (void)hipFree(cost);
+        if (order) (void)hipFree(order);
+    }
+};
+struct PlanKey {
+    int device;
+    void* stream;
+    uint32_t tiles_x, tiles;
+    int kind;  // kernel family
+    bool operator<(const PlanKey& o) const {
+        if (kind != o.kind) return kind < o.kind;
+        if (device != o.device) return device < o.device;
+        if (stream != o.stream) return stream < o.stream;
+        if (tiles_x != o.tiles_x) return tiles_x < o.tiles_x;
+        return tiles < o.tiles;
+    }
+};
+// Automatic kernel choice below 64 spp, by measurement.  Which of v3 (tile waves, longest-first order) and v4
+// (persistent, per-lane pixel queue) is faster there depends on the scene as much as on spp (config 2's scene
+// at 4 spp: v3 1.54 vs v4 1.77 ms; config 5's at 4 spp: 0.89 vs 0.65; config 3's at 8 spp: 14.1 vs 12.8,
+// profiles/r02_ab_v3_v4_low_spp.txt).  Both render the same bits, so the library times one frame of each
+// for a (device, stream, scene, frame shape, spp, depth, RNG mode) and keeps the faster: the first frame
+// runs v3 untimed (it builds the tile order), the second v3 timed, the third v4 timed, and the choice is
+// made once both timings have completed (until then: v4 below 32 spp, v3 from 32).
+struct AutoKey {
+    int device;
+    void* stream;
+    const void* scene;
+    uint32_t width, rows, spp, depth, philox;
+    bool operator<(const AutoKey& o) const {
+        return std::tie(device, stream, scene, width, rows, spp, depth, philox) <
+               std::tie(o.device, o.stream, o.scene, o.width, o.rows, o.spp, o.depth, o.philox);
+    }
+};
+struct AutoChoice {
+    int stage = 0;      // frames of the trial already launched
+    int chosen = -1;    // the decided variant
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // v3 start/end, v4 start/end
+    ~AutoChoice() {
+        for (hipEvent_t& e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+constexpr uint32_t kAutoSpp = 64;  // from here on v3 always (configs 2-4: 64-256 spp)
+std::mutex g_auto_mu;
+// never destroyed (holds HIP events, see g_plans)
+// entries held by shared_ptr: a frame being timed keeps its AutoChoice (and events) alive even if another
+// thread clears the map meanwhile
+std::map<AutoKey, std::shared_ptr<AutoChoice>>& g_auto = *new std::map<AutoKey, std::shared_ptr<AutoChoice>>();
+
+// never destroyed: plans free device memory, which must not run after the HIP runtime has shut down
+std::map<PlanKey, std::shared_ptr<TilePlan>>& g_plans = *new std::map<PlanKey, std::shared_ptr<TilePlan>>();
+std::mutex g_plans_mu;
+constexpr size_t kMaxPlans = 32;
+
+int acquire_plan(const PlanKey& key, hipStream_t s, std::shared_ptr<TilePlan>* out) {
+    std::lock_guard<std::mutex> lock(g_plans_mu);
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) {
+        if (g_plans.size() >= kMaxPlans) g_plans.clear();  // holders keep their plans alive
+        auto p = std::make_shared<TilePlan>();
+        void* c = nullptr;
+        void* o = nullptr;
+        int rc = hip_check(hipMalloc(&c, (size_t)key.tiles * 4), "rt_render: tile cost allocation");
+        p->cost = (uint32_t*)c;
+        if (rc == RT_OK) rc = hip_check(hipMalloc(&o, (size_t)key.tiles * 4), "rt_render: tile order allocation");
+        p->order = (uint32_t*)o;
+        if (rc == RT_OK) rc = hip_check(hipMemsetAsync(c, 0, (size_t)key.tiles * 4, s), "rt_render: tile cost reset");
+        if (rc != RT_OK) return rc;
+        it = g_plans.emplace(key, std::move(p)).first;
+    }
+    *out = it->second;
+    return RT_OK;
+}
+thread_local int g_persistent_waves = 0;  // 0: occupancy query
+
+constexpr size_t kLdsLimit = 160 * 1024;
+
+// Work-queue heads of the persistent kernel: a ring of counters per device, one slot per launch, zeroed
+// on the launch's stream right before it.  A slot is kQueueBytes (the kQueueCounters heads, up to 4 KB apart,
+// plus the exhausted-heads word) and is reused after kQueueSlots further persistent launches on that device:
+// a caller may keep at most kQueueSlots persistent launches in flight per device (rt_hip.h, rt_render).
+constexpr uint32_t kQueueSlots = 256;
+constexpr uint32_t kQueueMaxStride = 4096;  // bytes between heads (RT_TUNE_QUEUE_STRIDE)
+constexpr uint32_t kQueueBytes = (dev::kQueueCounters + 1u) * kQueueMaxStride;
+thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 queue heads
+thread_local int g_queue_chunk = 64;    // RT_TUNE_QUEUE_CHUNK: work indices per queue atomic
+constexpr int kMaxDevices = 64;
+struct QueueRing {
+    uint32_t* buf = nullptr;
+    std::atomic<uint32_t> next{0};
+    int cus = 0;
+};
+QueueRing g_queues[kMaxDevices];
+std::mutex g_queue_mu;
+
+int acquire_queue(int device, uint32_t** head, int* cus) {
+    if (device < 0 || device >= kMaxDevices) {
+        set_error("rt_render: device ordinal out of range");
+        return RT_ERR_DEVICE;
+    }
+    QueueRing& q = g_queues[device];
+    {
+        std::lock_guard<std::mutex> lock(g_queue_mu);
+        if (!q.buf) {
+            void* p = nullptr;
+            int rc = hip_check(hipMalloc(&p, (size_t)kQueueSlots * kQueueBytes), "rt_render: work queue allocation");
+            if (rc != RT_OK) return rc;
+            q.buf = (uint32_t*)p;
+            int n = 0;
+            rc = hip_check(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device),
+                           "rt_render: compute unit count");
+            if (rc != RT_OK) return rc;
+            q.cus = n;
+        }
+    }
+    *head = q.buf + (size_t)(q.next.fetch_add(1u) % kQueueSlots) * (kQueueBytes / 4u);
+    *cus = q.cus;
+    return RT_OK;
+}
+
+}  // namespace
+
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" {
+
+int rt_set_wave_trace(void* buffer) {
+    g_wave_trace = (unsigned long long*)buffer;
+    return RT_OK;
+}
+
+int rt_set_tile_order(const void* order) {
+    g_tile_order = (const uint32_t*)order;
+    return RT_OK;
+}
+
+int rt_set_timing(int enabled) {
+    g_timing = enabled != 0;
+    return RT_OK;
+}
+
+float rt_last_kernel_ms(void) { return g_last_ms; }
+
+float rt_last_launch_host_ms(void) { return g_last_host_ms; }
+
+// Benchmark/tuning knob: -1 = automatic, else an index into kVariants.  Returns the previous value.
+int rt_set_variant(int variant) {
+    int prev = g_variant;
+    g_variant = variant;
+    return prev;
+}
+
+int rt_last_variant(void) { return g_last_variant; }
+
+int rt_set_tuning(int key, int value) {
+    if (key == RT_TUNE_REGEN_THRESHOLD) {
+        if (value < 1 || value > 64) {
+            set_error("rt_set_tuning: regen threshold must be in [1, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_regen_threshold;
+        g_regen_threshold = value;
+        return prev;
+    }
+    if (key == RT_TUNE_LEAF_MAX) {
+        if (value < 1 || value > kLeafMax) {
+            set_error("rt_set_tuning: leaf max must be in [1, 4]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_leaf_max;
+        g_leaf_max = value;
+        return prev;
+    }
+    if (key == RT_TUNE_SAH_TRAVERSAL) {
+        if (value < 1 || value > 1000) {
+            set_error("rt_set_tuning: SAH traversal cost (x10) must be in [1, 1000]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_sah_traversal_x10;
+        g_sah_traversal_x10 = value;
+        return prev;
+    }
+    if (key == RT_TUNE_ADAPTIVE_ORDER) {
+        if (value < 0 || value > 1) {
+            set_error("rt_set_tuning: adaptive order must be 0 or 1");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_adaptive_order;
+        g_adaptive_order = value;
+        return prev;
+    }
+    if (key == RT_TUNE_TEXEL_LAYOUT) {
+        if (value != 3 && value != 4) {
+            set_error("rt_set_tuning: texel layout must be 3 (RGB8) or 4 (RGBA8)");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_texel_bytes;
+        g_texel_bytes = value;
+        return prev;
+    }
+    if (key == RT_TUNE_LDS_PAD) {
+        if (value < 0 || value > 65536 || value % 4) {
+            set_error("rt_set_tuning: LDS pad must be a multiple of 4 in [0, 65536]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_lds_pad;
+        g_lds_pad = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_CHUNK) {
+        if (value < 64 || value > 4096 || value % 64) {
+            set_error("rt_set_tuning: queue chunk must be a multiple of 64 in [64, 4096]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_chunk;
+        g_queue_chunk = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_STRIDE) {
+        if (value < 128 || value > (int)kQueueMaxStride || (value & (value - 1))) {
+            set_error("rt_set_tuning: queue head stride must be a power of two in [128, 4096] bytes");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_stride;
+        g_queue_stride = value;
+        return prev;
+    }
+    if (key == RT_TUNE_PERSISTENT_WAVES) {
+        if (value < 0 || value > 16) {
+            set_error("rt_set_tuning: persistent waves per SIMD must be in [0, 16]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_persistent_waves;
+        g_persistent_waves = value;
+        return prev;
+    }
+    set_error("rt_set_tuning: unknown key");
+    return RT_ERR_INVALID_ARGUMENT;
+}
+
+int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) {
+    if (!scene || !a) { set_error("rt_render: NULL scene or args"); return RT_ERR_INVALID_ARGUMENT; }
+    if (a->tiling.local_rows == 0 || a->width == 0 || a->height == 0) return RT_OK;  // nothing to render
+    const bool philox = (a->flags & RT_FLAG_RNG_PHILOX) != 0;
+    if (!a->state && !philox) { set_error("rt_render: state is NULL"); return RT_ERR_INVALID_ARGUMENT; }
+    if (a->reserved != 0 || a->reserved2 != 0) { set_error("rt_render: reserved fields must be 0"); return RT_ERR_INVALID_ARGUMENT; }
+    if (!a->pos && !a->radiance && !a->accum) { set_error("rt_render: no output buffer"); return RT_ERR_INVALID_ARGUMENT; }
+    if ((a->flags & RT_FLAG_ACCUMULATE) && !a->accum) { set_error("rt_render: ACCUMULATE without accum"); return RT_ERR_INVALID_ARGUMENT; }
+    if (a->width == 0 || a->height == 0) return RT_OK;
+    const rt_tiling& T = a->tiling;
+    if (T.band_rows == 0 || T.num_ranks == 0 || T.rank >= T.num_ranks) {
+        set_error("rt_render: invalid tiling");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    if (T.local_rows == 0) return RT_OK;
+    {
+        // the last local row must map into the image
+        uint32_t l = T.local_rows - 1, band = l / T.band_rows, within = l % T.band_rows;
+        uint64_t g = ((uint64_t)band * T.num_ranks + T.rank) * T.band_rows + within;
+        if (g >= a->height) { set_error("rt_render: tiling maps local rows outside the image"); return RT_ERR_INVALID_ARGUMENT; }
+    }
+    const DeviceScene& S = scene->dev;
+    if (S.depth > (uint32_t)dev::kStackMax) {
+        set_error("rt_render: BVH deeper than the traversal stack");
+        return RT_ERR_UNSUPPORTED;
+    }
+    dev::KParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.nodes = (const float4*)S.nodes;
+    P.nodes48 = (const float4*)S.nodes48;
+    P.refs = (const uint32_t*)S.refs;
+    P.prims = (const float4*)S.prims;
+    P.mats = (const float4*)S.mats;
+    P.imgs = (const int4*)S.imgs;
+    P.texels = (const uint8_t*)S.texels;
+    P.pos = a->pos;
+    P.radiance = (float4*)a->radiance;
+    P.accum = (float4*)a->accum;
+    P.state = (uint32_t*)a->state;
+    if (a->flags & RT_FLAG_STATE_SOA) {  // six planes of whole 8×8 tiles
+        const uint64_t plane = rt_soa_plane_words(a->width, T.local_rows);
+        if (plane > 0xffffffffull) {
+            set_error("rt_render: RT_FLAG_STATE_SOA needs < 2^32 pixels per rank");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        P.state_stride = (uint32_t)plane;
+    } else {
+        P.state_stride = 1u;
+    }
+    P.counters = (unsigned long long*)a->counters;
+    P.num_nodes = S.num_nodes;
+    P.num_prims = S.num_prims;
+    P.width = a->width;
+    P.height = a->height;
+    P.spp = a->samples_per_pixel;
+    P.max_depth = a->max_depth;
+    P.flags = a->flags;
+    P.band_rows = T.band_rows;
+    P.num_ranks = T.num_ranks;
+    P.rank = T.rank;
+    P.local_rows = T.local_rows;
+    P.tiles_x = 0;  // set below for the chosen workgroup shape
+    const bool faithful = (a->flags & RT_FLAG_FAITHFUL_GRID) != 0;
+    P.grid_w = faithful ? (a->width / 16) * 16 : a->width;
+    P.grid_h = faithful ? (a->height / 16) * 16 : a->height;
+    P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
+    P.regen_threshold = (uint32_t)g_regen_threshold;
+    P.rng_key_lo = (uint32_t)a->rng_seed;
+    P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
+    P.rng_frame = a->rng_frame;
+    P.wave_trace = g_wave_trace;
+    P.tile_order = g_tile_order;
+    // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
+    const rt_input_struct& in = a->inputs;
+    P.width_f = (float)a->width;
+    P.inv_width = 1.0f / P.width_f;
+    P.cx = (float)a->width / 2.0f;
+    P.cy = (float)a->height / 2.0f;
+    P.near_plane = in.near_plane;
+    P.far_plane = in.far_plane;
+    {
+        volatile float up[3] = {in.up[0], in.up[1], in.up[2]};
+        volatile float fw[3] = {in.orientation[0], in.orientation[1], in.orientation[2]};
+        // rightV = Normalize(Cross(upV, forwardV)) (Kernel.cu:133, Math.cuh:157-161, 225-229)
+        volatile float cx = up[1] * fw[2] - up[2] * fw[1];
+        volatile float t = up[0] * fw[2] - up[2] * fw[0];
+        volatile float cy = -t;
+        volatile float cz = up[0] * fw[1] - up[1] * fw[0];
+        volatile float d0 = cx * cx, d1 = cy * cy, d2 = cz * cz;
+        volatile float dd = d0 + d1;
+        dd = dd + d2;
+        volatile float s = std::sqrt((float)dd);
+        volatile float inv = 1.0f / s;
+        P.right[0] = inv * cx;
+        P.right[1] = inv * cy;
+        P.right[2] = inv * cz;
+        volatile float k10 = 1.0f / in.fov;
+        k10 = k10 * 10.0f;
+        for (int i = 0; i < 3; i++) {
+            P.origin[i] = in.origin[i];
+            P.up[i] = in.up[i];
+            P.fov_fwd[i] = in.fov * fw[i];
+            P.k10_fwd[i] = k10 * fw[i];
+            P.bg0[i] = in.background_start[i];
+            P.bg1[i] = in.background_end[i];
+        }
+    }
+
+    const bool count_tests = a->counters && (a->flags & RT_FLAG_COUNT_TESTS);
+    int variant = g_variant;
+    // auto: the fastest measured kernel per workload shape (profiles/r01d_*, r01e_*): the persistent v4 when a
+    // pixel has few paths (config 5: 1 spp, 0.51-0.54 vs 0.80 ms), otherwise v3 with the adaptive
+    // longest-first tile order and compact parking: 13 words of parked state + a depth + 2 stack fit config
+    // 2's wave in 5 KB of LDS, 8 waves per SIMD (config 2: 17.05 vs 17.8 ms with 15-word parking; config 3,
+    // depth 16: 365 vs 408 ms for v4).  Compact parking falls back to 15 words where its packed counters
+    // would overflow.
+    std::shared_ptr<AutoChoice> trial;  // this frame is timed for the automatic choice: events ev[trial_slot..+1]
+    int trial_slot = 0;
+    const bool automatic = variant < 0 || variant >= kNumVariants;
+    if (automatic) {
+        variant = a->samples_per_pixel < 32 ? kVarV4 : kVarV3Compact;
+        if (a->samples_per_pixel > 0 && a->samples_per_pixel < kAutoSpp && a->max_depth > 0) {
+            int device = 0;
+            (void)hipGetDevice(&device);
+            const AutoKey key{device, stream, scene, a->width, T.local_rows, a->samples_per_pixel, a->max_depth,
+                              philox ? 1u : 0u};
+            std::lock_guard<std::mutex> lock(g_auto_mu);
+            auto it = g_auto.find(key);
+            if (it == g_auto.end()) {
+                if (g_auto.size() >= 64) g_auto.clear();
+                it = g_auto.emplace(key, std::make_shared<AutoChoice>()).first;
+            }
+            const std::shared_ptr<AutoChoice> held = it->second;
+            AutoChoice& ac = *held;
+            if (ac.chosen >= 0) {
+                variant = ac.chosen;
+            } else if (ac.stage < 3) {
+                variant = ac.stage < 2 ? kVarV3Compact : kVarV4;
+                if (ac.stage >= 1) {
+                    trial_slot = ac.stage == 1 ? 0 : 2;
+                    if ((ac.ev[trial_slot] || hipEventCreate(&ac.ev[trial_slot]) == hipSuccess) &&
+                        (ac.ev[trial_slot + 1] || hipEventCreate(&ac.ev[trial_slot + 1]) == hipSuccess))
+                        trial = held;
+                }
+                ac.stage++;
+            } else if (ac.ev[1] && ac.ev[3] && hipEventQuery(ac.ev[1]) == hipSuccess &&
+                       hipEventQuery(ac.ev[3]) == hipSuccess) {
+                float t3 = -1.0f, t4 = -1.0f;
+                (void)hipEventElapsedTime(&t3, ac.ev[0], ac.ev[1]);
+                (void)hipEventElapsedTime(&t4, ac.ev[2], ac.ev[3]);
+                ac.chosen = (t3 >= 0.0f && t4 >= 0.0f && t4 < t3) ? kVarV4 : kVarV3Compact;
+                variant = ac.chosen;
+            } else if (!ac.ev[1] || !ac.ev[3]) {
+                ac.chosen = variant;  // no events: keep the static rule
+            }
+            (void)hipGetLastError();  // (hipEventQuery reports hipErrorNotReady while pending)
+        }
+    }
+    const bool packable =
+        a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u;
+    if (kVariants[variant].compact && !packable) variant = kVarV3;  // packed counters would overflow
+    if (kVariants[variant].kernel == 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
+        variant = packable ? kVarV3Compact : kVarV3;  // the persistent kernel assumes every pixel traces a ray
+    if (philox && kVariants[variant].stack != dev::STACK_LDS16)
+        variant = packable ? kVarV3Compact : kVarV3;  // the v1/v2 kernels have no Philox build
+    // Scenes whose references need 32 bits (S.wide_refs: >= 32767 nodes or >= 8192 primitives) run the WIDE builds
+    // of the compact v3 and of v4; the 15-word v3 has none: v2 / v1 there (no Philox build either).
+    bool wide = false;
+    if (kVariants[variant].stack == dev::STACK_LDS16 && S.wide_refs) {
+        if (variant == kVarV3) {
+            if (philox) {
+                set_error("rt_render: RT_FLAG_RNG_PHILOX on a scene with 32-bit references needs spp < 8192, "
+                          "max_depth < 64 and spp * max_depth < 8192");
+                return RT_ERR_UNSUPPORTED;
+            }
+            variant = S.depth <= 25u ? kVarV2 : kVarV1;  // 32-bit LDS stacks, or scratch if deep
+        } else {
+            wide = true;
+        }
+    }
+    const Variant& V = kVariants[variant];
+    const bool persistent = V.kernel == 4;
+    // near-first traversal holds at most one deferred child per level below the root
+    if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
+        set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
+        return RT_ERR_UNSUPPORTED;
+    }
+    // v3/v4: per wave, the parked path state + a 16-bit stack of depth + 2 entries: two sentinel pads, and
+    // a visit at level L (root = 1) holds at most L - 1 deferred children, so its unconditional write of
+    // the far child lands at index 2 + (L - 1) <= depth + 1 (the 128-B saving keeps config 2's wave
+    // inside 10 × 512 B of LDS)
+    const size_t wave_bytes = V.stack == dev::STACK_LDS16
+                                  ? (size_t)(persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
+                                        (size_t)(S.depth + 2) * 64 * (wide ? 4 : 2) + (size_t)g_lds_pad
+                                  : 0;
+    P.lds_wave_words = (uint32_t)(wave_bytes / 4);
+    size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes;
+    if (lds_bytes > kLdsLimit) {
+        set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
+        return RT_ERR_UNSUPPORTED;
+    }
+    KernelFn fn = pick(variant, count_tests, S.has_textures, philox, wide);
+    const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave
+    P.tiles_x = (a->width + tile - 1) / tile;
+    const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t grid = tiles;
+    if (persistent) {
+        int device = 0, cus = 0, per_cu = 0;
+        int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
+        if (rc == RT_OK) rc = acquire_queue(device, &P.work_counter, &cus);
+        if (rc == RT_OK)
+            rc = hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, V.block, lds_bytes),
+                           "rt_render: occupancy query");
+        if (rc != RT_OK) return rc;
+        P.work_total = tiles * 64u;
+        P.work_chunk = (uint32_t)g_queue_chunk;
+        P.queue_stride = (uint32_t)g_queue_stride / 4u;
+        P.work_per_counter = ((tiles * 64u + dev::kQueueCounters - 1u) / dev::kQueueCounters + P.work_chunk - 1u) /
+                             P.work_chunk * P.work_chunk;
+        if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
+        const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
+        grid = (uint32_t)(resident < grid ? resident : grid);
+        rc = hip_check(hipMemsetAsync(P.work_counter, 0, (size_t)(dev::kQueueCounters + 1u) * g_queue_stride, s),
+                       "rt_render: work queue reset");
+        if (rc != RT_OK) return rc;
+    }
+    P.num_tiles = tiles;
+    std::shared_ptr<TilePlan> plan;
+    if (V.kernel == 3 && g_adaptive_order && !g_tile_order) {
+        int device = 0;
+        int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
+        if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles, V.kernel}, s, &plan);
+        if (rc != RT_OK) return rc;
+        P.tile_cost = plan->cost;
+        P.tile_order = plan->valid.load() ? plan->order : nullptr;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing) {
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipEventRecord(e0, s);
+    }
+    g_last_variant = variant;
+    if (trial) (void)hipEventRecord(trial->ev[trial_slot], s);
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(V.block), lds_bytes, s, P);
+    int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
+    if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);  // the render kernel alone (v4 has no plan step)
+    if (rc == RT_OK && plan) {  // the next launch on this stream dispatches this frame's costliest tiles first
+        hipLaunchKernelGGL(dev::plan_order_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)plan->cost, plan->order,
+                           tiles);
+        rc = hip_check(hipGetLastError(), "rt_render: plan kernel launch", RT_ERR_LAUNCH);
+        if (rc == RT_OK) plan->valid.store(true);
+    }
+    if (g_timing) {
+        (void)hipEventRecord(e1, s);
+        if (rc == RT_OK && hipEventSynchronize(e1) == hipSuccess) {
+            float ms = -1.0f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            g_last_ms = ms;
+        } else {
+            g_last_ms = -1.0f;
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    return rc;
+}
+
+uint64_t rt_soa_plane_words(uint32_t width, uint32_t local_rows) {
+    return (((uint64_t)width + 7u) / 8u) * (((uint64_t)local_rows + 7u) / 8u) * 64u;
+}
+
+namespace {
+int render_init(void* d_state, uint32_t width, const rt_tiling* tiling, uint64_t seed_base, rt_stream stream,
+                uint32_t soa, const char* who) {  // soa: 0 = rt_curand_state, else the plane layout
+    if (!tiling) { set_error(std::string(who) + ": NULL tiling"); return RT_ERR_INVALID_ARGUMENT; }
+    if ((size_t)width * tiling->local_rows == 0) return RT_OK;  // nothing to seed
+    if (!d_state) { set_error(std::string(who) + ": NULL state"); return RT_ERR_INVALID_ARGUMENT; }
+    if (tiling->band_rows == 0 || tiling->num_ranks == 0 || tiling->rank >= tiling->num_ranks) {
+        set_error(std::string(who) + ": invalid tiling");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    const size_t n = (size_t)width * tiling->local_rows;
+    if (soa) {
+        const uint64_t plane = rt_soa_plane_words(width, tiling->local_rows);
+        if (plane > 0xffffffffull) {
+            set_error(std::string(who) + ": needs < 2^32 pixels per rank");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        soa = (uint32_t)plane;  // the kernel's plane stride
+    }
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(dev::render_init_kernel, dim3((unsigned)((n + dev::kBlock - 1) / dev::kBlock)), dim3(dev::kBlock), 0,
+                       (hipStream_t)stream, (uint32_t*)d_state, width, tiling->local_rows, tiling->band_rows,
+                       tiling->num_ranks, tiling->rank, (unsigned long long)seed_base, soa);
+    return hip_check(hipGetLastError(), (std::string(who) + ": kernel launch").c_str(), RT_ERR_LAUNCH);
+}
+}  // namespace
+
+int rt_render_init(rt_curand_state* d_state, uint32_t width, uint32_t height, const rt_tiling* tiling,
+                   uint64_t seed_base, rt_stream stream) {
+    (void)height;
+    return render_init(d_state, width, tiling, seed_base, stream, 0u, "rt_render_init");
+}
+
+int rt_render_init_soa(uint32_t* d_planes, uint32_t width, uint32_t height, const rt_tiling* tiling,
+                       uint64_t seed_base, rt_stream stream) {
+    (void)height;
+    return render_init(d_planes, width, tiling, seed_base, stream, 1u, "rt_render_init_soa");
+}
+
+// ----- reference-named drop-in launchers (synchronous, void) ----------------------------------------
+
+void LaunchRenderInit(rt_dim3 grid, rt_dim3 block, unsigned int window_width, unsigned int window_height,
+                      rt_curand_state* d_rand_state) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(dev::render_init_grid_kernel, dim3(grid.x, grid.y, grid.z), dim3(block.x, block.y, block.z), 0, 0,
+                       (uint32_t*)d_rand_state, window_width, window_height);
+    if (hip_check(hipGetLastError(), "LaunchRenderInit: kernel launch", RT_ERR_LAUNCH) == RT_OK)
+        hip_check(hipDeviceSynchronize(), "LaunchRenderInit: hipDeviceSynchronize");
+}
+
+void LaunchRandInit(rt_curand_state* d_rand_state2) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(dev::rand_init_kernel, dim3(1), dim3(1), 0, 0, (uint32_t*)d_rand_state2);
+    if (hip_check(hipGetLastError(), "LaunchRandInit: kernel launch", RT_ERR_LAUNCH) == RT_OK)
+        hip_check(hipDeviceSynchronize(), "LaunchRandInit: hipDeviceSynchronize");
+}
+
+void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int image_height,
+                  const unsigned int samples_per_pixel, const unsigned int max_depth, const void* world,
+                  rt_curand_state* d_rand_state, rt_input_struct inputs) {
+    // The viewer mutates the graph in place between frames: the cache re-flattens it on
+    // every call and updates the device scene by what changed (reference_scene_for_launch, api.cpp).
+    std::shared_ptr<rt_scene> cached;  // held until the frame is done (another thread may evict the entry)
+    double host_ms = 0.0;
+    const int rc = reference_scene_for_launch(world, &cached, &host_ms);
+    g_last_host_ms = (float)host_ms;
+    if (rc != RT_OK) return;
+    rt_render_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.pos = pos;
+    a.state = d_rand_state;
+    a.width = image_width;
+    a.height = image_height;
+    a.samples_per_pixel = samples_per_pixel;
+    a.max_depth = max_depth;
+    a.flags = RT_FLAG_FAITHFUL_GRID;
+    a.tiling.band_rows = image_height ? image_height : 1;
+    a.tiling.num_ranks = 1;
+    a.tiling.rank = 0;
+    a.tiling.local_rows = image_height;
+    a.inputs = inputs;
+    if (rt_render(cached.get(), &a, nullptr) != RT_OK) return;
+    hip_check(hipDeviceSynchronize(), "LaunchKernel: hipDeviceSynchronize");  // Kernel.cu:190
+}
+
+}  // extern "C"
