@@ -769,8 +769,6 @@ struct RngPhilox {
 };
 
 // Block `blk` of the lane's stream: philox10(ctr = {blk, frame, pixel, 0}, key = seed) into s.r0..r3.
-// The key and frame are re-read from the kernel arguments here (scalar loads) rather than carried: held across
-// the kernel, the unrolled key schedule cost 12 SGPR spills (into VGPR lanes).
 __device__ __forceinline__ void philox_block(RngPhilox& s, uint32_t blk) {
     KParamsC* q = kparams_reload();
     uint32_t c0 = blk, c1 = q->rng_frame, c2 = s.pix, c3 = 0u;
@@ -1614,7 +1612,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
-            if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
+            if (ended) {
                 col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
                          __uint_as_float(park[(PK_COL + 2) * 64]));
                 v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
@@ -1954,7 +1952,7 @@ KernelFn v4_pick(bool count, bool tex) {
 }
 
 constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
-constexpr int kPhiloxCompactWaves = 8;  // ... of the non-texture Philox build of variant 3
+constexpr int kPhiloxCompactWaves = 7;  // ... of the non-texture Philox build of variant 3
 
 KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
     if (wide) {  // 32-bit references: builds of the compact v3 and of v4 only (rt_render maps wide scenes there)
@@ -1967,10 +1965,9 @@ KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
     case kVarV2: return count ? dev::render_kernel_v2<true> : dev::render_kernel_v2<false>;
     case kVarV3: return philox ? v3_pick<1, true>(count, tex) : v3_pick<1>(count, tex);
     case kVarV3Compact:
-        // Waves per SIMD by registers (profiles/r02_ab_builds_c2.txt, profiles/r03_ab_philox.txt): XORWOW held to 64
-        // VGPRs (8 waves, 8 B of cold spills) 16.98 vs 17.25 ms at the compiler's 68; Philox, once its key is read
-        // per block and the colour sum stays parked during shading, to 64 as well (20 B of cold spills): 20.24 vs
-        // 20.6 ms at 7 waves
+        // Waves per SIMD by registers (profiles/r02_ab_builds_c2.txt): XORWOW held to 64 VGPRs (8 waves,
+        // 28 B of cold spills) 16.98 vs 17.25 ms at the compiler's 68; Philox held to 72 (7 waves) 21.5 vs
+        // 21.9 ms at 75, while 8 waves (64 VGPRs, 40 B of spills) ran 22.6 ms
         if (philox)
             return tex ? v3_pick<1, true, true>(count, true) : v3_pick<kPhiloxCompactWaves, true, true>(count, false);
         return tex ? v3_pick<1, false, true>(count, true) : v3_pick<kXorwowCompactWaves, false, true>(count, false);

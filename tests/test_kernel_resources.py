@@ -1,10 +1,10 @@
 """Resource budget of the kernels the automatic choice runs (CPU: reads the gfx950 code object's metadata).
 
 A private array that LLVM materialises in scratch (it happened to the Philox word select: scratch loads on
-every draw, +8 % frame time) or a register count past 72 (7 waves per SIMD) is a performance regression
+every draw, +8 % frame time) or a register count past 64 (8 waves per SIMD) is a performance regression
 the parity tests cannot see.  This test pins "no scratch" for the v3 (variants 2, 3) and v4 (variant 4)
 kernels in both RNG modes, with and without texture support, and <= 72 VGPRs for the v3 kernels of
-untextured scenes (<= 64 for the XORWOW build of variant 3, the headline kernel; the texture-capable and persistent kernels run at 85-98
+untextured scenes (<= 64 for the XORWOW and Philox builds of variant 3, the headline kernels; the texture-capable and persistent kernels run at 85-98
 VGPRs, 5 waves per SIMD, measured in DESIGN.md)."""
 import os
 import re
@@ -18,11 +18,11 @@ LIB = os.path.join(ROOT, "cudaraytracer_amd", "librt_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 # render_kernel_v3<COUNT_TESTS=false, W, TEX, PHILOX, COMPACT, WIDE> (variants 2 and 3; the untextured compact
-# 16-bit-reference builds are held to 8 (XORWOW) / 7 (Philox) waves per SIMD by registers, render.hip
+# 16-bit-reference builds are held to 8 waves per SIMD by registers (both RNG modes), render.hip
 # k*CompactWaves; the 32-bit-reference (WIDE) builds exist for the compact v3 and v4 only)
 # render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX, WIDE> (variant 4)
 def _v3(t, p, c, wd=0):
-    w = (8 if not p else 7) if (c and not t and not wd) else 1
+    w = 8 if (c and not t and not wd) else 1
     return f"_ZN2rt3dev16render_kernel_v3ILb0ELi{w}ELb{t}ELb{p}ELb{c}ELb{wd}EEEvNS0_7KParamsE"
 
 
@@ -33,7 +33,7 @@ def _v4(t, p, wd=0):
 HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + [_v4(t, p) for t in (0, 1) for p in (0, 1)] + \
       [_v3(t, p, 1, 1) for t in (0, 1) for p in (0, 1)] + [_v4(t, p, 1) for t in (0, 1) for p in (0, 1)]
 # register-held builds: a few bytes of cold spills (measured faster than the compiler's register count)
-SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 24}
+SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 32}
 
 
 def kernel_metadata(tmp_path):
@@ -67,4 +67,4 @@ def test_hot_kernels_register_and_scratch_budget(tmp_path):
             assert meta[k]["vgpr_count"] <= 72, (k, meta[k])
     # the default kernel of untextured many-sample frames (variant 3, XORWOW) at 8 waves per SIMD
     assert meta[_v3(0, 0, 1)]["vgpr_count"] <= 64
-    assert meta[_v3(0, 1, 1)]["vgpr_count"] <= 72
+    assert meta[_v3(0, 1, 1)]["vgpr_count"] <= 64
