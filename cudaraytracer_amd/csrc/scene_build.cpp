@@ -113,6 +113,9 @@ struct Builder {
     };
     std::vector<Node> nodes;
     uint32_t max_depth = 0;
+    // > 0: every leaf at a depth <= depth_limit (root = 1).  Each split then keeps both sides within what a
+    // subtree of the remaining depth can hold (leaf_max << levels left), choosing the best SAH split among those.
+    uint32_t depth_limit = 0;
 
     Box range_box(int b, int e) const {
         Box r;
@@ -130,6 +133,13 @@ struct Builder {
         if (depth > max_depth) max_depth = depth;
         const bool must_split = depth == 1;  // the root is always an internal node (see build_root)
         if (n <= 1 && !must_split) return make_leaf(b, e);
+        int lo_split = 1, hi_split = n - 1;  // allowed left-side sizes
+        if (depth_limit) {
+            if (depth >= depth_limit) return make_leaf(b, e);  // n <= leaf_max here by the capacities above
+            const int64_t cap = (int64_t)leaf_max << (depth_limit - depth - 1);
+            lo_split = (int)std::max<int64_t>(1, n - cap);
+            hi_split = (int)std::min<int64_t>(n - 1, cap);
+        }
         // Full-sweep SAH over the three centroid axes.
         float best_cost = INFINITY;
         int best_axis = -1, best_split = -1;
@@ -148,6 +158,7 @@ struct Builder {
             acc.empty();
             for (int i = 1; i < n; i++) {
                 acc.grow(prims[tmp[i - 1]].box);
+                if (i < lo_split || i > hi_split) continue;
                 float cost = acc.area() * (float)i + right_area[i] * (float)(n - i);
                 if (cost < best_cost) { best_cost = cost; best_axis = axis; best_split = i; }
             }
@@ -157,7 +168,7 @@ struct Builder {
         if (!must_split && n <= leaf_max && best_cost + traversal * all.area() >= leaf_cost) return make_leaf(b, e);
         if (best_axis < 0) {  // every candidate cost overflowed (boxes at the end of the float range): object median
             best_axis = 0;
-            best_split = n / 2;
+            best_split = std::min(std::max(n / 2, lo_split), hi_split);
         }
         std::stable_sort(order.begin() + b, order.begin() + e, [&](int x, int y) {
             return prims[x].centroid[best_axis] < prims[y].centroid[best_axis];
@@ -372,6 +383,19 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
                 B = std::move(T);
                 break;
             }
+        }
+        // still too deep (thousands of primitives): SAH splits under capacity limits that bound the depth — to
+        // kOccupancyDepth when the primitives fit its leaves (8192 at leaf size 4: every 16-bit-reference scene),
+        // else to one level above the shallowest tree that holds them (the LDS stack grows with the depth)
+        uint32_t dmin = 1;
+        while (((size_t)B.leaf_max << (dmin - 1)) < B.prims.size()) dmin++;
+        const uint32_t target = std::max<uint32_t>(kOccupancyDepth, dmin + (dmin > kOccupancyDepth ? 1u : 0u));
+        if (B.max_depth > target) {
+            Builder T = B;
+            T.traversal = base;
+            T.depth_limit = target;
+            T.build_root();
+            B = std::move(T);
         }
     }
     out->num_prims = (uint32_t)B.prims.size();
