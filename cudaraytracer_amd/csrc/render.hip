@@ -647,12 +647,13 @@ __device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32
         a.z = a.z + col.z;
         a.w = a.w + (float)P.spp;
         P.accum[pix] = a;
-        c = divs(mk(a.x, a.y, a.z), a.w);
+        c = divs_rn(mk(a.x, a.y, a.z), a.w, recip_in_range(a.w));  // = divs(sum, a.w) bit for bit
     } else {
-        c = divs(col, (float)P.spp);
+        const float n = (float)P.spp;
+        c = divs_rn(col, n, recip_in_range(n));  // = divs(col, spp) bit for bit (IEEE division outside its range)
     }
     if (P.radiance) P.radiance[pix] = make_float4(c.x, c.y, c.z, 1.0f);
-    if (P.pos) P.pos[pix] = rgb_to_int(255.0f * sqrtf(c.x), 255.0f * sqrtf(c.y), 255.0f * sqrtf(c.z));
+    if (P.pos) P.pos[pix] = rgb_to_int(255.0f * sqrt_fast(c.x), 255.0f * sqrt_fast(c.y), 255.0f * sqrt_fast(c.z));
 }
 
 template <bool COUNT_TESTS>
