@@ -206,9 +206,10 @@ struct KParams {
     uint32_t* work_counter;    // v4: the frame's kQueueCounters queue heads, queue_stride words apart (zeroed before
                                // the launch), then the exhausted-heads word
     uint32_t queue_stride;     // v4: words between queue heads (RT_TUNE_QUEUE_STRIDE; 32 = 128 B)
-    uint32_t work_chunk;       // v4: work indices a wave takes per atomic (RT_TUNE_QUEUE_CHUNK; a multiple of 64)
+    uint32_t work_chunk;       // v4: work indices a wave takes per atomic while its head has plenty left
+                               // (RT_TUNE_QUEUE_CHUNK; a multiple of 64); 64 near the head's end
     uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
-    uint32_t work_per_counter; // v4: indices per queue head (a multiple of work_chunk): head k owns [k·n, (k+1)·n)
+    uint32_t work_per_counter; // v4: indices per queue head (a multiple of 64): head k owns [k·n, (k+1)·n)
     uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
     uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
     unsigned long long* wave_trace;  // diagnostic: v3 per tile {start, end}; v4 per wave {start, queue drained,
@@ -1705,6 +1706,10 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     // wave-uniform: the queue head the wave draws from (one of kQueueCounters, each owning a contiguous
     // range of the frame; a wave moves on to the next head when its own is exhausted) and heads tried
     uint32_t qc = blockIdx.x % kQueueCounters, qtried = 0u;
+    // wave-uniform: the head's remaining indices as of this wave's last grab from it.  Chunks of work_chunk
+    // indices (fewer atomics, wider spatially coherent runs of pixels) while plenty remain, then 64: the
+    // indices a wave has taken but not started keep only that wave busy once the queue is dry (the frame's tail)
+    uint32_t head_left = 0xffffffffu;
     uint32_t wave_pixels = 0u;           // wave-uniform: pixels this wave has taken
     const uint32_t threshold = P.regen_threshold;
     const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
@@ -1748,7 +1753,8 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                 if (wq_next >= wq_end) {
                     const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
                     uint32_t base = 0u;
-                    if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, P.work_chunk);
+                    const uint32_t want = head_left > 4u * P.work_chunk ? P.work_chunk : 64u;
+                    if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, want);
                     base = __builtin_amdgcn_readlane(base, leader);
                     const uint32_t idx = qc * P.work_per_counter + base;
                     if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
@@ -1765,10 +1771,13 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
                         const uint32_t live = ~done & kQueueAllDone;        // (nonzero here)
                         const uint32_t above = live & ~((2u << qc) - 1u);   // live heads after qc
                         qc = (uint32_t)__builtin_ctz(above ? above : live);
+                        head_left = 0u;  // (unknown: small chunks until the first grab there)
                         continue;
                     }
                     wq_next = idx;
-                    wq_end = idx + P.work_chunk;
+                    // (a chunk ends at its head's range: a head's range is a multiple of 64, not of work_chunk)
+                    wq_end = idx + min(want, P.work_per_counter - base);
+                    head_left = P.work_per_counter - base - min(want, P.work_per_counter - base);
                 }
                 const uint32_t avail = wq_end - wq_next;
                 const uint32_t rank =
@@ -2455,8 +2464,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.work_total = tiles * 64u;
         P.work_chunk = (uint32_t)g_queue_chunk;
         P.queue_stride = (uint32_t)g_queue_stride / 4u;
-        P.work_per_counter = ((tiles * 64u + dev::kQueueCounters - 1u) / dev::kQueueCounters + P.work_chunk - 1u) /
-                             P.work_chunk * P.work_chunk;
+        P.work_per_counter = (tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
         if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
         grid = (uint32_t)(resident < grid ? resident : grid);

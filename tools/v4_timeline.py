@@ -94,15 +94,19 @@ for name, kw in cases:
     show(name + " [untraced]", run(traced=False, **kw))
 
 if args.sweep:
-    base = dict(ds=ds5, cfg=c5, spp=1, depth=4, flags=acc)
-    for chunk in (64, 128, 256, 512):
-        for stride in (128, 4096):
+    for name, base in (("c5", dict(ds=ds5, cfg=c5, spp=1, depth=4, flags=acc)),
+                       ("c2 1 spp", dict(ds=ds2, cfg=scenes.CONFIGS["c2"], spp=1, depth=8, flags=0))):
+        for chunk in (64, 128, 256, 512, 1024):
+            for stride in (128, 4096):
+                prev_c = lib().rt_set_tuning(7, chunk)
+                prev_s = lib().rt_set_tuning(8, stride)
+                show(f"{name} chunk {chunk} stride {stride} B", run(**base))
+                lib().rt_set_tuning(7, prev_c)
+                lib().rt_set_tuning(8, prev_s)
+    for w in (3, 4, 5):
+        for chunk in (64, 256):
+            prev = lib().rt_set_tuning(2, w)
             prev_c = lib().rt_set_tuning(7, chunk)
-            prev_s = lib().rt_set_tuning(8, stride)
-            show(f"c5 chunk {chunk} stride {stride} B", run(**base))
+            show(f"c5 persistent waves/SIMD {w} chunk {chunk}", run(ds=ds5, cfg=c5, spp=1, depth=4, flags=acc))
+            lib().rt_set_tuning(2, prev)
             lib().rt_set_tuning(7, prev_c)
-            lib().rt_set_tuning(8, prev_s)
-    for w in (2, 4, 6, 8):
-        prev = lib().rt_set_tuning(2, w)
-        show(f"c5 persistent waves/SIMD {w}", run(**base))
-        lib().rt_set_tuning(2, prev)
