@@ -114,6 +114,15 @@ __device__ __forceinline__ f3 divs_rn(const f3 v, const float s, const float y) 
     }
     return divs(v, s);
 }
+// x / a bit for bit: div_rn from RN(1/a) inside its proven range (|a| in [2^-40, 2^40], |x| in [2^-100, 2^100] or
+// x == +0), the IEEE division (a branch no lane usually takes) elsewhere.
+__device__ __forceinline__ float fdiv(const float x, const float a) {
+    const float m = fabsf(x);
+    float r;
+    if (in_rcp_range(a) && ((m >= 0x1p-100f && m <= 0x1p100f) || __float_as_uint(x) == 0u)) r = div_rn(x, a, rcp_rn(a));
+    else r = x / a;
+    return r;
+}
 __device__ __forceinline__ float recip_in_range(const float s) {
     return in_rcp_range(s) ? rcp_rn(s) : 0.0f;
 }
@@ -385,8 +394,8 @@ __device__ __forceinline__ float rt_asin_poly(const float x) {  // |x| <= 0.5
 }
 __device__ __forceinline__ float rt_acosf(float x) {
     x = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
-    if (x < -0.5f) return 0x1.921fb6p+1f - 2.0f * rt_asin_poly(sqrtf(0.5f * (1.0f + x)));
-    if (x > 0.5f) return 2.0f * rt_asin_poly(sqrtf(0.5f * (1.0f - x)));
+    if (x < -0.5f) return 0x1.921fb6p+1f - 2.0f * rt_asin_poly(sqrt_fast(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * rt_asin_poly(sqrt_fast(0.5f * (1.0f - x)));
     return 0x1.921fb6p+0f - rt_asin_poly(x);
 }
 __device__ __forceinline__ float rt_atan_poly(const float x) {  // |x| <= tan(pi/8)
@@ -394,15 +403,15 @@ __device__ __forceinline__ float rt_atan_poly(const float x) {  // |x| <= tan(pi
     return (((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x + x;
 }
 __device__ __forceinline__ float rt_atan01(const float t) {  // t in [0, 1]
-    if (t > 0.41421356f) return 0x1.921fb6p-1f + rt_atan_poly((t - 1.0f) / (t + 1.0f));
+    if (t > 0.41421356f) return 0x1.921fb6p-1f + rt_atan_poly(fdiv(t - 1.0f, t + 1.0f));
     return rt_atan_poly(t);
 }
 __device__ __forceinline__ float rt_atan2f(const float y, const float x) {
     const float ax = fabsf(x), ay = fabsf(y);
     float r;
     if (ax == 0.0f && ay == 0.0f) r = 0.0f;
-    else if (ay <= ax) r = rt_atan01(ay / ax);
-    else r = 0x1.921fb6p+0f - rt_atan01(ax / ay);
+    else if (ay <= ax) r = rt_atan01(fdiv(ay, ax));
+    else r = 0x1.921fb6p+0f - rt_atan01(fdiv(ax, ay));
     if (__builtin_signbit(x)) r = 0x1.921fb6p+1f - r;  // IEEE atan2: x < 0 or -0
     return __builtin_signbit(y) ? -r : r;
 }
@@ -521,16 +530,16 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         if (TEX && ttype == RT_IMAGE && mtype != RT_DIELECTRIC) {  // GetSphereUV (Hittable.cuh:119-125)
             const float theta = rt_acosf(-normal.y);
             const float phi = rt_atan2f(-normal.z, normal.x) + 3.141592654f;
-            hu = phi / (2 * 3.141592654f);
-            hv = theta / 3.141592654f;
+            hu = fdiv(phi, 2 * 3.141592654f);
+            hv = fdiv(theta, 3.141592654f);
         }
     } else {  // hit record of *Rect::Hit (Hittable.cuh:155-166)
         const float oa = type == RT_YZRECT ? ro.y : ro.x, da = type == RT_YZRECT ? rd.y : rd.x;
         const float ob = type == RT_XYRECT ? ro.y : ro.z, db = type == RT_XYRECT ? rd.y : rd.z;
         const float xx = oa + t * da;
         const float yy = ob + t * db;
-        hu = (xx - p0.y) / (p0.z - p0.y);
-        hv = (yy - p0.w) / (p1.x - p0.w);
+        hu = fdiv(xx - p0.y, p0.z - p0.y);
+        hv = fdiv(yy - p0.w, p1.x - p0.w);
         const f3 outward = type == RT_XYRECT ? mk(0.0f, 0.0f, 1.0f)
                            : type == RT_XZRECT ? mk(0.0f, 1.0f, 0.0f)
                                                : mk(1.0f, 0.0f, 0.0f);
