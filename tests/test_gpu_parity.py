@@ -719,3 +719,27 @@ def test_automatic_choice_times_both_kernels_and_keeps_the_bits(config, spp):
     lib().rt_set_variant(-1)
     r.render(ds, 64, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
     assert lib().rt_last_variant() == 3  # from 64 spp: v3
+
+
+@pytest.mark.parametrize("chunk, stride", [(64, 128), (128, 4096), (256, 128), (1024, 4096)])
+def test_persistent_queue_knobs_change_schedule_not_pixels(chunk, stride):
+    """The v4 work queue's chunk size (RT_TUNE_QUEUE_CHUNK, adaptive per head) and head spacing
+    (RT_TUNE_QUEUE_STRIDE) decide which wave renders which pixel, never what it computes: every setting gives the
+    oracle's image, ray count and advanced RNG states."""
+    case = CASE_BY_NAME["c2_rtiow_ragged_100x37_s4"]
+    cfg = case.cfg()
+    g = load_golden(case.name)
+    prev_c, prev_s = lib().rt_set_tuning(7, chunk), lib().rt_set_tuning(8, stride)
+    lib().rt_set_variant(4)
+    try:
+        r = Renderer(cfg.width, cfg.height)
+        r.render_init()
+        r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
+        torch.cuda.synchronize()
+        assert lib().rt_last_variant() == 4
+    finally:
+        lib().rt_set_variant(-1)
+        lib().rt_set_tuning(7, prev_c)
+        lib().rt_set_tuning(8, prev_s)
+    np.testing.assert_array_equal(r.image(), g["pos"])
+    assert int(r.counters[0]) == int(g["counters"][0])
