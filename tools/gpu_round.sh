@@ -23,7 +23,7 @@ for step in $STEPS; do
       tail -1 gpurun_out/bench.log ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
-        python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench_prof.log 2>&1 || exit $? ;;
+        python3 bench.py --no-cpu-baseline --no-config-lines ${BENCH_ARGS:-} > gpurun_out/bench_prof.log 2>&1 || exit $? ;;
     benchcfg)  # driver-shaped lines for BASELINE configs 3 and 5
       for cfg in c5 c3; do
         timeout -k 10 400 python bench.py --config $cfg --steps ${CFG_STEPS:-5} --warmup 2 ${BENCH_ARGS:-} \
