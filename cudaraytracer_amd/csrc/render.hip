@@ -225,9 +225,7 @@ struct KParams {
                                      // end, pixels} of s_memrealtime (100 MHz)
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
-    uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile (v5: regions)
-    uint32_t region_tiles;           // v5: consecutive 8×8 tiles per region (one wave)
-    uint32_t image_tiles;            // v5: tiles of the (local) image
+    uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
 };
 
 constexpr int kStackMax = 64;
@@ -1838,116 +1836,6 @@ __global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
-// ---------------------------------------------------------------------------------------------------
-// v5: v3 with per-lane pixel refill inside a region of adjacent tiles.
-//   v3 binds a lane to one pixel for the wave's lifetime, so a lane whose pixel is done idles until the
-//   wave's slowest pixel finishes (6.7 of 64 lanes per node iteration on C2).  A v5 wave owns
-//   P.region_tiles consecutive 8×8 tiles (row-major tile order) and hands the region's pixels to its lanes as
-//   theirs finish — a wave-uniform counter and ballot + mbcnt ranks, no atomics — so the idle tail comes once
-//   per region instead of once per tile while a wave's pixels stay spatially close (v4's frame-wide queue
-//   mixes distant pixels).  Regions are dispatched longest-first like v3's tiles.  Parked state as compact
-//   v3 (13 words); the frame's ray count is kept per wave (lanes that start a ray, counted by ballot).
-//   Every pixel still runs its own samples on its own RNG stream, so the image is v3's bit for bit.
-//   Requires spp ≥ 1, max_depth ≥ 1 and compact parking's limits (rt_render uses v3 otherwise).
-// ---------------------------------------------------------------------------------------------------
-template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false>
-__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v5(const KParams P) {
-    using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
-    using Entry = typename RefW<false>::Entry;
-    extern __shared__ float4 lds[];
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t* const wl = (uint32_t*)lds;
-    uint32_t* const park = wl + lane;
-    Entry* const stk = reinterpret_cast<Entry*>(wl + PK_WORDS_COMPACT * 64) + lane;
-    const __amdgpu_buffer_rsrc_t nrsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
-    const float4* __restrict__ prims = P.prims;
-    const uint32_t slot = blockIdx.x;
-    const uint32_t region = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
-    const uint32_t first = region * P.region_tiles * 64u;  // the region's first work index (work_pixel numbering)
-    const uint32_t total = min(P.region_tiles * 64u, P.image_tiles * 64u - first);
-    const bool rtl = P.rius_rtl != 0;
-    stk[0] = (Entry)RefW<false>::kSentinel;
-    stk[64] = (Entry)RefW<false>::kSentinel;
-
-    Counts cnt{0, 0, 0, 0, 0, 0, 0};
-    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
-    Cursor c{(int)RefW<false>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_NEED};
-    uint32_t x = 0u, g = 0u, pix = 0u;  // the lane's pixel
-    uint32_t next = 0u;                 // wave-uniform: region work indices handed out
-    uint32_t wave_pixels = 0u, wave_rays = 0u;
-    const uint32_t threshold = P.regen_threshold;
-    const uint64_t w_start = __builtin_amdgcn_s_memtime();
-    bool shading = false;
-    while (true) {
-        if (c.mode == MODE_TRAV)
-            v3_traverse<COUNT_TESTS, NODES_48, PK_WORDS_COMPACT * 256u, false>(nrsrc, P.nodes48, P.refs, prims, stk,
-                                                                              threshold, ro, rd, c, cnt);
-        shading = c.mode == MODE_SHADE;
-        if (shading) {
-            R rng;
-            f3 col, att;
-            uint32_t sample, depth, rays;
-            v3_unpark<true, false>(park, rng, col, att, sample, depth, rays);
-            f3 contrib;
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
-            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
-                ended = true;
-                contrib = mk(0.0f, 0.0f, 0.0f);
-            }
-            if (ended) {
-                col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
-                         __uint_as_float(park[(PK_COL + 2) * 64]));
-                v3_next_sample<false>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
-                if (c.mode == MODE_DONE) {  // the pixel is done (Kernel.cu:149-157): write it, take another
-                    write_pixel(P, pix, state_at(P, pix), rng, col);
-                    c.mode = MODE_NEED;
-                } else {
-                    park[(PK_COL + 0) * 64] = __float_as_uint(col.x);
-                    park[(PK_COL + 1) * 64] = __float_as_uint(col.y);
-                    park[(PK_COL + 2) * 64] = __float_as_uint(col.z);
-                }
-            } else {
-                v3_start_trace<false>(P.num_nodes, c, rays);
-            }
-            if (c.mode != MODE_NEED) v3_park<true, false>(park, rng, col, att, sample, depth, 0u);
-        }
-        wave_rays += (uint32_t)__popcll(__ballot(shading && c.mode == MODE_TRAV));  // rays started
-        uint64_t needm = __ballot(c.mode == MODE_NEED);
-        if (needm != 0) {
-            bool took = false;  // this lane started a new pixel (and its first ray)
-            while (needm != 0 && next < total) {
-                const uint32_t rank =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
-                if (c.mode == MODE_NEED && next + rank < total) {
-                    if (work_pixel(P, first + next + rank, x, g, pix)) {
-                        took = true;
-                        R rng = begin_rng<R>(state_at(P, pix), P.state_stride, g * P.width + x);
-                        f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
-                        uint32_t sample = (uint32_t)-1, depth = 0u, rays = 0u;
-                        v3_next_sample<false>(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
-                        v3_park<true>(park, rng, col, att, sample, depth, 0u);
-                    }
-                }
-                next += min((uint32_t)__popcll(needm), total - next);
-                needm = __ballot(c.mode == MODE_NEED);
-            }
-            const uint32_t started = (uint32_t)__popcll(__ballot(took));
-            wave_pixels += started;
-            wave_rays += started;  // each new pixel's first camera ray
-            if (c.mode == MODE_NEED) c.mode = MODE_DONE;
-        }
-        if (__ballot(c.mode != MODE_DONE) == 0) break;
-    }
-    if (P.tile_cost && wave_leader()) {  // this region's cost for the next launch's longest-first order
-        const uint64_t t = (__builtin_amdgcn_s_memtime() - w_start) >> 8;
-        P.tile_cost[region] = t > 0xffffffffull ? 0xffffffffu : (uint32_t)t;
-    }
-    cnt.rays = __lane_id() == 0 ? wave_rays : 0u;
-    cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;
-    flush_counts<COUNT_TESTS>(P, cnt);
-}
-
 // RenderInit (Kernel.cu:166-176): curand_init(seed_base + global_pixel_index, 0, 0).
 __device__ __forceinline__ void curand_init_state(unsigned long long seed, uint32_t* st, uint32_t k = 1u) {
     const uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
@@ -2058,7 +1946,6 @@ using KernelFn = void (*)(const dev::KParams);
 //   4  v4: persistent work queue, 64-B nodes      — timed against 3 below 64 spp (a compact-parking, 48-B-node,
 //         longest-first-ordered v4 measured slower on C2, C3 and C5: profiles/r02_ab_v3_v4compact_c2.txt,
 //         profiles/r02_configs_v345.txt)
-//   5  v5: v3 compact with per-lane refill inside a region of RT_TUNE_REGION_TILES tiles
 struct Variant {
     int stack;        // StackKind
     int lds_depth;    // v2: LDS stack entries per lane
@@ -2068,10 +1955,10 @@ struct Variant {
 };
 constexpr Variant kVariants[] = {
     {dev::STACK_SCRATCH, 0, 256, 1, false}, {dev::STACK_LDS, 24, 64, 2, false}, {dev::STACK_LDS16, 0, 64, 3, false},
-    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false}, {dev::STACK_LDS16, 0, 64, 5, true},
+    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
-constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4, kVarV5 = 5;
+constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4;
 
 template <int W, bool PH = false, bool C = false, bool WD = false>
 KernelFn v3_pick(bool count, bool tex) {
@@ -2088,12 +1975,6 @@ KernelFn v4_pick(bool count, bool tex) {
 constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
 constexpr int kPhiloxCompactWaves = 8;  // ... of the non-texture Philox build of variant 3
 
-template <int W, bool PH = false>
-KernelFn v5_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v5<true, 1, true, PH> : dev::render_kernel_v5<false, 1, true, PH>;
-    return count ? dev::render_kernel_v5<true, W, false, PH> : dev::render_kernel_v5<false, W, false, PH>;
-}
-
 KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
     if (wide) {  // 32-bit references: builds of the compact v3 and of v4 only (rt_render maps wide scenes there)
         if (variant == kVarV3Compact)
@@ -2104,7 +1985,6 @@ KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
     case kVarV1: return count ? dev::render_kernel<true> : dev::render_kernel<false>;
     case kVarV2: return count ? dev::render_kernel_v2<true> : dev::render_kernel_v2<false>;
     case kVarV3: return philox ? v3_pick<1, true>(count, tex) : v3_pick<1>(count, tex);
-    case kVarV5: return philox ? v5_pick<kPhiloxCompactWaves, true>(count, tex) : v5_pick<kXorwowCompactWaves>(count, tex);
     case kVarV3Compact:
         // Waves per SIMD by registers (profiles/r02_ab_builds_c2.txt, profiles/r03_ab_philox.txt): XORWOW held to 64
         // VGPRs (8 waves, 8 B of cold spills) 16.98 vs 17.25 ms at the compiler's 68; Philox, once its key is read
@@ -2122,7 +2002,6 @@ thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupa
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
-thread_local int g_region_tiles = 2;                        // RT_TUNE_REGION_TILES (v5)
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
@@ -2363,15 +2242,6 @@ int rt_set_tuning(int key, int value) {
         g_queue_stride = value;
         return prev;
     }
-    if (key == RT_TUNE_REGION_TILES) {
-        if (value < 1 || value > 64) {
-            set_error("rt_set_tuning: region tiles must be in [1, 64]");
-            return RT_ERR_INVALID_ARGUMENT;
-        }
-        int prev = g_region_tiles;
-        g_region_tiles = value;
-        return prev;
-    }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
         if (value < 0 || value > 16) {
             set_error("rt_set_tuning: persistent waves per SIMD must be in [0, 16]");
@@ -2546,9 +2416,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool packable =
         a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u;
     if (kVariants[variant].compact && !packable) variant = kVarV3;  // packed counters would overflow
-    if (kVariants[variant].kernel >= 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
-        variant = packable ? kVarV3Compact : kVarV3;  // v4/v5 assume every pixel traces a ray
-    if (variant == kVarV5 && S.wide_refs) variant = kVarV3Compact;  // (no 32-bit-reference build)
+    if (kVariants[variant].kernel == 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
+        variant = packable ? kVarV3Compact : kVarV3;  // the persistent kernel assumes every pixel traces a ray
     if (philox && kVariants[variant].stack != dev::STACK_LDS16)
         variant = packable ? kVarV3Compact : kVarV3;  // the v1/v2 kernels have no Philox build
     // Scenes whose references need 32 bits (S.wide_refs: >= 32767 nodes or >= 8192 primitives) run the WIDE builds
@@ -2593,9 +2462,6 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
     hipStream_t s = (hipStream_t)stream;
     uint32_t grid = tiles;
-    P.image_tiles = tiles;
-    P.region_tiles = V.kernel == 5 ? (uint32_t)g_region_tiles : 1u;
-    if (V.kernel == 5) grid = (tiles + P.region_tiles - 1u) / P.region_tiles;  // one wave per region
     if (persistent) {
         int device = 0, cus = 0, per_cu = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
@@ -2615,14 +2481,12 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                        "rt_render: work queue reset");
         if (rc != RT_OK) return rc;
     }
-    const uint32_t slots = V.kernel == 5 ? grid : tiles;  // v5 plans regions
-    P.num_tiles = slots;
+    P.num_tiles = tiles;
     std::shared_ptr<TilePlan> plan;
-    if ((V.kernel == 3 || V.kernel == 5) && g_adaptive_order && !g_tile_order) {
+    if (V.kernel == 3 && g_adaptive_order && !g_tile_order) {
         int device = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
-        if (rc == RT_OK)
-            rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x * P.region_tiles, slots, V.kernel}, s, &plan);
+        if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles, V.kernel}, s, &plan);
         if (rc != RT_OK) return rc;
         P.tile_cost = plan->cost;
         P.tile_order = plan->valid.load() ? plan->order : nullptr;
@@ -2641,7 +2505,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);  // the render kernel alone (v4 has no plan step)
     if (rc == RT_OK && plan) {  // the next launch on this stream dispatches this frame's costliest tiles first
         hipLaunchKernelGGL(dev::plan_order_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)plan->cost, plan->order,
-                           slots);
+                           tiles);
         rc = hip_check(hipGetLastError(), "rt_render: plan kernel launch", RT_ERR_LAUNCH);
         if (rc == RT_OK) plan->valid.store(true);
     }

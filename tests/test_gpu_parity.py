@@ -23,9 +23,9 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = list(range(6))  # every kernel librt_hip.so ships (kVariants in render.hip)
-# v3 (2), v3 compact parking (3), persistent v4 (4), region-refill v5 (5)
-KEY_VARIANTS = [2, 3, 4, 5]
+VARIANTS = list(range(5))  # every kernel librt_hip.so ships (kVariants in render.hip)
+# v3 (2), v3 compact parking (3), persistent v4 (4)
+KEY_VARIANTS = [2, 3, 4]
 
 
 @pytest.fixture(autouse=True)
@@ -63,35 +63,6 @@ def test_bit_exact_vs_golden(case, variant):
     assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes()
     assert int(r.counters[0]) == int(g["counters"][0])  # rays
     assert int(r.counters[3]) == int(g["counters"][3])  # primary samples
-
-
-@pytest.mark.parametrize("region", [1, 3, 7, 64])
-@pytest.mark.parametrize("rng", ["xorwow", "philox"])
-def test_region_refill_sizes_keep_the_pixels(region, rng):
-    """v5 hands a region's pixels to lanes as theirs finish: any region size (ragged last region, regions wider
-    than the frame) renders the golden image, states and counts of the pixel-per-lane kernels."""
-    case = CASE_BY_NAME["c2_rtiow_ragged_100x37_s4"]
-    prev = lib().rt_set_tuning(abi.RT_TUNE_REGION_TILES, region)
-    try:
-        if rng == "xorwow":
-            g = load_golden(case.name)
-            r, _, _ = _render(case, 5)
-            np.testing.assert_array_equal(r.image(), g["pos"])
-            assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes()
-            assert int(r.counters[0]) == int(g["counters"][0]) and int(r.counters[3]) == int(g["counters"][3])
-        else:
-            cfg = case.cfg()
-            imgs = []
-            for v in (3, 5):
-                lib().rt_set_variant(v)
-                r = Renderer(cfg.width, cfg.height, rng="philox")
-                r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs())
-                torch.cuda.synchronize()
-                imgs.append((r.image(), int(r.counters[0])))
-            np.testing.assert_array_equal(imgs[0][0], imgs[1][0])
-            assert imgs[0][1] == imgs[1][1]
-    finally:
-        lib().rt_set_tuning(abi.RT_TUNE_REGION_TILES, prev)
 
 
 @pytest.mark.parametrize("case", [CASE_BY_NAME["c2_rtiow_192x112_s16"], CASE_BY_NAME["c3_cornell_128_s16"]],

@@ -14,7 +14,7 @@ ap.add_argument("--spp", type=int, default=0)
 ap.add_argument("--thresholds", default="40", help="regen thresholds to try for resumable variants (>= 8)")
 ap.add_argument("--leafmax", default="4", help="BVH leaf sizes to try (RT_TUNE_LEAF_MAX)")
 ap.add_argument("--pwaves", default="0", help="persistent grid waves/SIMD to try (RT_TUNE_PERSISTENT_WAVES)")
-ap.add_argument("--regions", default="2", help="v5 tiles per region to try (RT_TUNE_REGION_TILES)")
+ap.add_argument("--regions", default="2", help="v5 tiles per region to try (RT_TUNE_REGION_TILES; a build with ab_src/v5_region_refill.patch)")
 ap.add_argument("--sah", default="16", help="SAH traversal costs x10 to try (RT_TUNE_SAH_TRAVERSAL)")
 ap.add_argument("--rng", default="xorwow", choices=("xorwow", "philox"))
 args = ap.parse_args()
