@@ -768,14 +768,16 @@ __device__ __forceinline__ Rng load_rng(const uint32_t* st, uint32_t k) {
 
 // ---------------------------------------------------------------------------------------------------
 // Perf-mode RNG (RT_FLAG_RNG_PHILOX): hipRAND/rocRAND Philox4x32-10 (rocrand_philox4x32_10.h:270-303,
-// rocrand_uniform.h:65-68, 239-242).  The pixel's stream is rocrand_init(seed, subsequence = global pixel
-// index, offset = frame << 34): draw n of the frame is word n & 3 of philox10(ctr = {n >> 2, frame,
-// pixel, 0}, key = seed), generated four at a time.  Nothing per pixel lives in HBM: the lane holds the
-// draw index, the current block of four words and the pixel index (six words, as the XORWOW state);
-// key and frame are launch-uniform kernel arguments.
+// rocrand_uniform.h:65-68, 281-284).  The pixel's stream is rocrand_init(seed, subsequence = global
+// pixel index, offset = frame << 34), consumed one block per draw group with rocrand_uniform4: each group
+// of k <= 3 consecutive draws of the reference (camera jitter 2, RandomInUnitSphere attempt 3, dielectric 1)
+// takes the first k words of the stream's next block, philox10(ctr = {g, frame, pixel, 0}, key = seed) for
+// group g of the frame.  A group never spans two blocks, so no word is selected at a lane-varying offset and
+// every group generates exactly one block; nothing per pixel lives in HBM and only the group counter is
+// carried (plus the pixel index); key and frame are launch-uniform kernel arguments.
 // ---------------------------------------------------------------------------------------------------
 struct RngPhilox {
-    uint32_t n, r0, r1, r2, r3, pix;
+    uint32_t n, r0, r1, r2, r3, pix;  // n: the next group's block; r0..r3: the current block (not carried)
     uint32_t k0, k1, frame;  // launch-uniform key and frame, read once when the stream is (un)parked
 };
 
@@ -807,48 +809,21 @@ __device__ __forceinline__ float philox_to_uniform(uint32_t x) {
     return __builtin_fmaf((float)x, 2.3283064e-10f, 2.3283064e-10f);  // 2^-32 + x·2^-32 (exact product)
 }
 
-// Word j (0..3) of the current block.
-// (Two selects on the index bits: LLVM turned the equivalent compare chain into a private array with
-// a lane-varying index, i.e. scratch stores and loads on every draw.)
-__device__ __forceinline__ uint32_t philox_word(const RngPhilox& s, uint32_t j) {
-    const bool odd = (j & 1u) != 0u, high = (j & 2u) != 0u;
-    const uint32_t lo = odd ? s.r1 : s.r0, hi = odd ? s.r3 : s.r2;
-    return high ? hi : lo;
-}
-
+// A one-draw group (the dielectric's ξ, Material.cuh:131): word 0 of the next block.
 __device__ __forceinline__ float uniform(RngPhilox& s) {
-    if ((s.n & 3u) == 0u) philox_block(s, s.n >> 2);
-    const float u = philox_to_uniform(philox_word(s, s.n & 3u));
-    s.n++;
-    return u;
+    philox_block(s, s.n++);
+    return philox_to_uniform(s.r0);
 }
-
-// k (2 or 3) consecutive draws with at most one block generation: the words left in the current block
-// (none when n is a multiple of 4) come first, then the next block.
-template <int K>
-__device__ __forceinline__ void philox_group(RngPhilox& s, uint32_t* out) {
-    const uint32_t j = s.n & 3u;
-    const uint32_t left = j == 0u ? 0u : 4u - j;  // unused words of the current block
-    uint32_t old[3];
-#pragma unroll
-    for (int i = 0; i < K; i++) old[i] = philox_word(s, (j + (uint32_t)i) & 3u);
-    if (left < (uint32_t)K) philox_block(s, (s.n + left) >> 2);
-#pragma unroll
-    for (int i = 0; i < K; i++) out[i] = (uint32_t)i < left ? old[i] : philox_word(s, (uint32_t)i - left);
-    s.n += (uint32_t)K;
+__device__ __forceinline__ void draw2(RngPhilox& s, float& a, float& b) {  // camera jitter (Kernel.cu:139-140)
+    philox_block(s, s.n++);
+    a = philox_to_uniform(s.r0);
+    b = philox_to_uniform(s.r1);
 }
-__device__ __forceinline__ void draw2(RngPhilox& s, float& a, float& b) {
-    uint32_t w[2];
-    philox_group<2>(s, w);
-    a = philox_to_uniform(w[0]);
-    b = philox_to_uniform(w[1]);
-}
-__device__ __forceinline__ void draw3(RngPhilox& s, float& a, float& b, float& c) {
-    uint32_t w[3];
-    philox_group<3>(s, w);
-    a = philox_to_uniform(w[0]);
-    b = philox_to_uniform(w[1]);
-    c = philox_to_uniform(w[2]);
+__device__ __forceinline__ void draw3(RngPhilox& s, float& a, float& b, float& c) {  // Random() (Math.cuh:233)
+    philox_block(s, s.n++);
+    a = philox_to_uniform(s.r0);
+    b = philox_to_uniform(s.r1);
+    c = philox_to_uniform(s.r2);
 }
 
 __device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPhilox&) {}  // stateless in HBM
@@ -1196,12 +1171,8 @@ __device__ __forceinline__ void park_rng(uint32_t* park, const Rng& r) {
     park[(PK_RNG + 4) * 64] = r.v3;
     park[(PK_RNG + 5) * 64] = r.v4;
 }
-__device__ __forceinline__ void park_rng(uint32_t* park, const RngPhilox& r) {
+__device__ __forceinline__ void park_rng(uint32_t* park, const RngPhilox& r) {  // the block is not carried
     park[(PK_RNG + 0) * 64] = r.n;
-    park[(PK_RNG + 1) * 64] = r.r0;
-    park[(PK_RNG + 2) * 64] = r.r1;
-    park[(PK_RNG + 3) * 64] = r.r2;
-    park[(PK_RNG + 4) * 64] = r.r3;
     park[(PK_RNG + 5) * 64] = r.pix;
 }
 __device__ __forceinline__ void unpark_rng(const uint32_t* park, Rng& r) {
@@ -1210,8 +1181,7 @@ __device__ __forceinline__ void unpark_rng(const uint32_t* park, Rng& r) {
 }
 __device__ __forceinline__ void unpark_rng(const uint32_t* park, RngPhilox& r) {
     KParamsC* q = kparams_reload();
-    r = RngPhilox{park[(PK_RNG + 0) * 64], park[(PK_RNG + 1) * 64], park[(PK_RNG + 2) * 64],
-                  park[(PK_RNG + 3) * 64], park[(PK_RNG + 4) * 64], park[(PK_RNG + 5) * 64],
+    r = RngPhilox{park[(PK_RNG + 0) * 64], 0u, 0u, 0u, 0u, park[(PK_RNG + 5) * 64],
                   q->rng_key_lo, q->rng_key_hi, q->rng_frame};
 }
 

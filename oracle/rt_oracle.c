@@ -117,9 +117,12 @@ float orc_curand_uniform(rt_curand_state* s) {
 /* Philox4x32-10: the perf-mode RNG BASELINE.json's north_star names ("hiprand (Philox) per-pixel   */
 /* state").  Restates rocRAND's philox4x32_10_engine (/opt/rocm/include/rocrand/                    */
 /* rocrand_philox4x32_10.h:270-303, the Random123 round) and rocrand_uniform (rocrand_uniform.h:    */
-/* 65-68, 239-242).  A pixel's stream is rocrand_init(seed, subsequence = global pixel index,        */
-/* offset = frame << 34): draw n of a frame is word n & 3 of philox10(ctr = {n >> 2, frame, pixel,  */
-/* 0}, key = {seed lo, seed hi}).  Pinned by tests/golden/philox_kat.json (rocRAND's own engine).   */
+/* 65-68, 281-284).            A pixel's stream is rocrand_init(seed, subsequence = global pixel      */
+/* index, offset = frame << 34), consumed one block per draw group (rocrand_uniform4): each group   */
+/* of k <= 3 consecutive draws of the reference (camera jitter Kernel.cu:139-140, Random()          */
+/* Math.cuh:233, the dielectric's Material.cuh:131) takes the first k words of the next block,      */
+/* philox10(ctr = {g, frame, pixel, 0}, key = {seed lo, seed hi}) for the frame's group g (the      */
+/* kernel's RngPhilox, render.hip).  Pinned by tests/golden/philox_kat.json (rocRAND's own engine). */
 /* ---------------------------------------------------------------------------------------------- */
 void orc_philox4x32_10(const unsigned int ctr_in[4], const unsigned int key_in[2], unsigned int out[4]) {
     unsigned int c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
@@ -158,6 +161,12 @@ typedef struct {
     unsigned int key[2], frame, pixel, n, r[4];
 } orc_rng;
 
+/* Start of a draw group: a Philox stream moves to the next block's first word (the rest of the current
+ * block is skipped); the XORWOW stream is sequential. */
+static inline void orc_group(orc_rng* g) {
+    if (g->philox) g->n = (g->n + 3u) & ~3u;
+}
+
 static float orc_uniform(orc_rng* g) {
     if (!g->philox) return orc_curand_uniform(g->xs);
     if ((g->n & 3u) == 0u) {
@@ -171,6 +180,7 @@ static float orc_uniform(orc_rng* g) {
 static inline v3 random_in_unit_sphere(orc_rng* st, int order, int* draws) {
     v3 p;
     do {
+        orc_group(st);
         float a = orc_uniform(st), b = orc_uniform(st), c = orc_uniform(st);
         v3 r = order == 0 ? mk(a, b, c) : mk(c, b, a);
         *draws += 3;
@@ -600,6 +610,7 @@ static int scatter(const orc_scene* s, const rt_material_desc* m, v3 ro, v3 rd, 
         }
         *draws += 1;
         *so = rec->p;
+        orc_group(st);
         *sd = orc_uniform(st) < reflect_prob ? reflected : refracted;
         return 1;
     }
@@ -705,6 +716,7 @@ void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, float* a
             }
             v3 col = mk(0.0f, 0.0f, 0.0f);
             for (unsigned smp = 0; smp < spp; smp++) {
+                orc_group(&g);
                 float u = ((float)((float)x - center.x) + orc_uniform(&g)) / (float)width;
                 float v = ((float)(center.y - (float)y) + orc_uniform(&g)) / (float)width;
                 v3 dist = add(scale(u, right), scale(v, up));

@@ -28,8 +28,9 @@ void orc_curand_init(unsigned long long seed, rt_curand_state* state);
 unsigned int orc_curand(rt_curand_state* state);
 float orc_curand_uniform(rt_curand_state* state);
 
-/* Philox4x32-10 (rocRAND philox4x32_10_engine / rocrand_uniform): ten rounds of the Random123 function,
- * and draw n of the (seed, pixel, frame) stream the perf-mode kernel uses (RT_FLAG_RNG_PHILOX). */
+/* Philox4x32-10 (rocRAND philox4x32_10_engine / rocrand_uniform): ten rounds of the Random123 function, and
+ * draw n of the sequential (seed, pixel, frame) stream; the perf-mode kernel (RT_FLAG_RNG_PHILOX) takes one
+ * block of it per draw group (rt_oracle.c). */
 void orc_philox4x32_10(const unsigned int ctr[4], const unsigned int key[2], unsigned int out[4]);
 float orc_philox_uniform_at(unsigned long long seed, unsigned int pixel, unsigned int frame, unsigned int n);
 

@@ -44,7 +44,9 @@ def digest(a: np.ndarray) -> bytes:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest()
 
 
-def main() -> None:
+def main(philox_only: bool = False) -> None:
+    if philox_only:  # python tests/golden/make_golden.py --philox-only
+        return philox_goldens()
     with open(os.path.join(HERE, "xorwow_kat.json"), "w") as f:
         json.dump(xorwow_kat(), f, indent=1)
     for which in range(5):
@@ -73,6 +75,10 @@ def main() -> None:
             texture_sha256=np.frombuffer(digest(np.concatenate([np.asarray(i).ravel() for i in sc.images])
                                                 if sc.images else np.zeros(0, np.uint8)), np.uint8))
         print(case.name, pos.shape, cnt.rays, flush=True)
+    philox_goldens()
+
+
+def philox_goldens() -> None:
     for case, frame in PHILOX_CASES:
         cfg = case.cfg()
         sc = scenes.builtin(cfg.scene)
@@ -88,4 +94,4 @@ def main() -> None:
 
 
 if __name__ == "__main__":
-    main()
+    main(philox_only="--philox-only" in sys.argv)
