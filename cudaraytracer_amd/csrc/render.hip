@@ -1659,8 +1659,8 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
     return true;
 }
 
-template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false>
-__global__ __launch_bounds__(64) void render_kernel_v4(const KParams P) {
+template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false, int WAVES_PER_SIMD = 1>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     using Entry = typename RefW<WIDE>::Entry;
     extern __shared__ float4 lds[];
@@ -1936,9 +1936,15 @@ KernelFn v3_pick(bool count, bool tex) {
     return count ? dev::render_kernel_v3<true, W, false, PH, C, WD> : dev::render_kernel_v3<false, W, false, PH, C, WD>;
 }
 
+// __launch_bounds__ waves per SIMD of the textured v4 build (config 5): the compiler's 98 VGPRs (4 waves/SIMD).  The
+// config-5 frame is not occupancy-bound: held to 5 / 6 / 8 waves it runs 0.30 / 0.33 / 0.51 ms against 0.293
+// (profiles/r03g_ab_v4_tex_waves.txt; 6 and 8 spill to scratch)
+constexpr int kV4TexWaves = 1;
 template <bool PH = false, bool WD = false>
 KernelFn v4_pick(bool count, bool tex) {
-    if (tex) return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH, WD> : dev::render_kernel_v4<false, true, dev::NODES_64, PH, WD>;
+    if (tex)
+        return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH, WD>
+                     : dev::render_kernel_v4<false, true, dev::NODES_64, PH, WD, kV4TexWaves>;
     return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH, WD> : dev::render_kernel_v4<false, false, dev::NODES_64, PH, WD>;
 }
 
