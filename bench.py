@@ -9,7 +9,9 @@ kernel itself (one closest-hit query = one iteration of color()'s loop, Kernel.c
   --config c2 (default, the BASELINE metric): N = 1 renders config 2 (1920×1080, 64 spp, depth 8, RTIOW
       final scene).  N > 1 (one process per GPU) is weak scaling: the image grows to round(1920·√N) ×
       round(1080·√N) (same camera and field of view, ≈2.07 M pixels per GPU), split in block-cyclic 16-row
-      bands, and every step ends with the RCCL gather to rank 0.
+      bands; every frame is gathered to rank 0 over RCCL on the collective's own stream while the next frame
+      renders (parallel.BandGather; the last frame's gather is inside the timed region, gather_ms is the part
+      of it the render stream waited for).
   --config c3: BASELINE config 3 (3840×2160, 256 spp, depth 16, Cornell box), one GPU.
   --config c4: BASELINE config 4 as configured, strong scaling: one 7680×4320, 128 spp, depth 8 RTIOW frame
       split over the N ranks in 16-row bands (N = 1 renders all of it) + the RCCL gather, whose time is
@@ -331,13 +333,18 @@ def run_rank(args) -> dict | None:
         r.reset_accumulation()
         return scenes.camera_inputs(pos, fwd, cfg.fov)
 
+    # multi-rank: frame k's gather runs on the collective's stream while frame k + 1 renders (parallel.BandGather)
+    gatherer = parallel.BandGather(cfg.width, cfg.height, band) if world > 1 else None
+
     def step():
         r.render(scene, cfg.spp, cfg.depth, frame_inputs(), flags=frame_flags)
         if world > 1:
-            parallel.gather_bands(r.pos, cfg.width, cfg.height, band, reuse=True)
+            gatherer.start(r.pos)
 
     for _ in range(args.warmup):
         step()
+    if world > 1:
+        gatherer.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -353,8 +360,10 @@ def run_rank(args) -> dict | None:
         r.render(scene, cfg.spp, cfg.depth, frame_inputs(), flags=frame_flags)
         ev[i][1].record(stream)
         if world > 1:
-            parallel.gather_bands(r.pos, cfg.width, cfg.height, band, reuse=True)
+            gatherer.start(r.pos)  # waits (stream-side) for frame i - 1's gather, then starts frame i's
         ev[i][2].record(stream)
+    if world > 1:
+        gatherer.finish()  # the last frame's gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -96,3 +96,45 @@ def gather_bands(local: torch.Tensor, width: int, height: int, band_rows: int, d
     if via_host:
         return full.to(local.device)
     return full if reuse else full.clone()
+
+
+class BandGather:
+    """Pipelined per-frame gather (the bench's multi-rank step): start(local) enqueues frame k's gather on the
+    collective's own stream and returns at once, so the caller's next render overlaps it; the next start (or
+    finish) makes the caller's stream wait for frame k's gather and unshuffles it on `dst`.  The send buffer is
+    refilled only after that wait, so a gather never reads a frame being rendered.  Device tensors under gloo
+    (one-GPU rehearsals) are gathered synchronously inside start; CPU tensors under gloo take the pipelined
+    path (tests/test_distributed.py)."""
+
+    def __init__(self, width: int, height: int, band_rows: int, dst: int = 0, group=None):
+        self.width, self.height, self.band_rows, self.dst, self.group = width, height, band_rows, dst, group
+        self.work = None
+        self.bufs = None
+
+    def start(self, local: torch.Tensor) -> None:
+        self.finish()
+        group = self.group
+        if local.is_cuda and dist.get_backend(group) == "gloo":  # device buffers staged through the host
+            self.result = gather_bands(local, self.width, self.height, self.band_rows, self.dst, group, reuse=True)
+            return
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        counts = local_row_counts(self.height, self.band_rows, world)
+        key = (group, world, rank, self.dst, max(counts), self.width, self.height, self.band_rows, local.dtype,
+               str(local.device), "pipelined")
+        self.bufs = _buffers(key, world, rank, self.dst, max(counts), self.width, self.height, local.dtype,
+                             local.device)
+        send, recv, _ = self.bufs
+        send[: local.numel()].copy_(local.reshape(-1))
+        self.work = dist.gather(send, recv, dst=self.dst, group=group, async_op=True)
+
+    def finish(self) -> torch.Tensor | None:
+        """The last started frame's (H, W) image on dst (None elsewhere); the caller's stream waits for it."""
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            _, recv, full = self.bufs
+            self.result = None
+            if dist.get_rank(self.group) == self.dst:
+                unshuffle_into(full, recv, self.height, self.width, self.band_rows)
+                self.result = full
+        return getattr(self, "result", None)

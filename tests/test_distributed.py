@@ -43,6 +43,47 @@ def _worker(rank: int, world: int, port: int, band_rows: int, out_path: str) -> 
     dist.destroy_process_group()
 
 
+def _pipelined_worker(rank: int, world: int, port: int, band_rows: int, out_path: str) -> None:
+    """BandGather as bench.py drives it: frame k's gather is started, frame k + 1 is "rendered" (the local
+    buffer overwritten) before frame k is finished; rank 0 keeps every finished frame."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from cudaraytracer_amd import parallel
+    from cudaraytracer_amd.renderer import band_rows_of
+
+    parallel.init_process_group("gloo")
+    width, height = 5, 37
+    rows = torch.tensor(band_rows_of(height, band_rows, world, rank), dtype=torch.int64)
+    local = torch.empty(len(rows) * width, dtype=torch.int64)
+    g = parallel.BandGather(width, height, band_rows)
+    frames = []
+    for k in range(4):
+        local.copy_((rows[:, None] * width + torch.arange(width) + 1000 * k).reshape(-1))  # frame k
+        if k:
+            prev = g.finish()
+            if rank == 0:
+                frames.append(prev.clone())
+        g.start(local)
+    last = g.finish()
+    if rank == 0:
+        frames.append(last.clone())
+        np.save(out_path, torch.stack(frames).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world, band_rows", [(2, 16), (3, 4)])
+def test_pipelined_band_gather_keeps_frames_apart(tmp_path, world, band_rows):
+    out = str(tmp_path / "frames.npy")
+    mp.start_processes(_pipelined_worker, args=(world, _free_port(), band_rows, out), nprocs=world,
+                       start_method="spawn")
+    frames = np.load(out)
+    base = np.arange(37 * 5).reshape(37, 5)
+    assert frames.shape == (4, 37, 5)
+    for k in range(4):
+        np.testing.assert_array_equal(frames[k], base + 1000 * k)
+
+
 @pytest.mark.parametrize("world, band_rows", [(2, 16), (2, 5), (3, 16)])
 def test_gather_bands_reassembles_the_frame(tmp_path, world, band_rows):
     sys.path.insert(0, ROOT)
