@@ -93,6 +93,8 @@ def parse_args(argv=None):
                     help="single-process multi-device split through the rt_tiled C ABI, e.g. 0,1,2,3 (or 0,0 on one GPU)")
     ap.add_argument("--no-config-lines", action="store_true",
                     help="N=1 --config c2: skip the BASELINE config 3 and 5 figures attached to the headline line")
+    ap.add_argument("--tune", default="",
+                    help="rt_set_tuning overrides as key=value[,key=value] (rt_tuning_key in include/rt_hip.h)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank launch: N gloo ranks gather synthetic bands (no GPU)")
     return ap.parse_args(argv)
@@ -303,6 +305,10 @@ def run_rank(args) -> dict | None:
         s = math.sqrt(world)
         cfg = cfg.scaled(int(round(cfg.width * s)), int(round(cfg.height * s)))
     lib().rt_set_variant(args.variant)
+    for kv in filter(None, args.tune.split(",")):
+        k, v = (int(x) for x in kv.split("="))
+        if lib().rt_set_tuning(k, v) < 0:
+            raise SystemExit(f"bench.py: rt_set_tuning({k}, {v}) refused")
     n_gpus = distinct_devices(world, device)
 
     band = parallel.DEFAULT_BAND_ROWS if world > 1 else cfg.height
@@ -341,7 +347,10 @@ def run_rank(args) -> dict | None:
         if world > 1:
             gatherer.start(r.pos)
 
-    for _ in range(args.warmup):
+    # below 64 spp the library times v3 and v4 on the first frames and then keeps the faster (rt_render's
+    # automatic choice): at least 4 untimed frames so the timed ones run the chosen kernel
+    warmup = max(args.warmup, 4) if cfg.spp < 64 and args.variant < 0 else args.warmup
+    for _ in range(warmup):
         step()
     if world > 1:
         gatherer.finish()
@@ -387,7 +396,7 @@ def run_rank(args) -> dict | None:
             "n_gpus": n_gpus,
             "world_size": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",

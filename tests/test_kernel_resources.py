@@ -20,14 +20,14 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 # render_kernel_v3<COUNT_TESTS=false, W, TEX, PHILOX, COMPACT, WIDE> (variants 2 and 3; the untextured compact
 # 16-bit-reference builds are held to 8 waves per SIMD by registers (both RNG modes), render.hip
 # k*CompactWaves; the 32-bit-reference (WIDE) builds exist for the compact v3 and v4 only)
-# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX, WIDE> (variant 4)
+# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX, WIDE, WAVES_PER_SIMD=1> (variant 4)
 def _v3(t, p, c, wd=0):
     w = 8 if (c and not t and not wd) else 1
     return f"_ZN2rt3dev16render_kernel_v3ILb0ELi{w}ELb{t}ELb{p}ELb{c}ELb{wd}EEEvNS0_7KParamsE"
 
 
 def _v4(t, p, wd=0):
-    return f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}ELb{wd}EEEvNS0_7KParamsE"
+    return f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}ELb{wd}ELi1EEEvNS0_7KParamsE"
 
 
 HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + [_v4(t, p) for t in (0, 1) for p in (0, 1)] + \
