@@ -10,6 +10,8 @@ Derived fields (MI355X: 8 XCDs, 256 CUs, 1024 SIMDs; SQ_* counters aggregate ove
   avg_waves_per_simd       = 4 SQ_WAVE_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8)
   valu_lane_utilization    = SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)
   ta_busy_frac_per_cu      = TA_TA_BUSY_sum / 256 / (GRBM_GUI_ACTIVE / 8)
+  valu_insts_per_simd_cycle = SQ_INSTS_VALU / (1024 x GRBM_GUI_ACTIVE / 8)   (wave instructions issued per SIMD
+                              per cycle: at a 2-4 cycle issue cost per wave64 instruction, ~0.4 is a full VALU port)
 Algorithmic HBM bytes per pixel: XORWOW 24 B state in + 24 B out + 4 B RGBA8; Philox 4 B; config 5 (progressive)
 adds the float4 accumulator read and written (32 B)."""
 import collections, csv, glob, json, os, sys
@@ -57,6 +59,9 @@ def summary(out, rng):
         "valu_lane_utilization": round(p["SQ_THREAD_CYCLES_VALU"] / (64.0 * p["SQ_ACTIVE_INST_VALU"]), 4),
         "avg_waves_per_simd": round(4.0 * p["SQ_WAVE_CYCLES"] / (1024.0 * gui), 3),
         "ta_busy_frac_per_cu": round(p["TA_TA_BUSY_sum"] / 256.0 / gui, 4),
+        "sq_insts_valu": int(p["SQ_INSTS_VALU"]),
+        "valu_insts_per_simd_cycle": round(p["SQ_INSTS_VALU"] / (1024.0 * gui), 4),
+        "gpu_cycles": int(gui),
     }
 
 
