@@ -769,12 +769,12 @@ __device__ __forceinline__ Rng load_rng(const uint32_t* st, uint32_t k) {
 // ---------------------------------------------------------------------------------------------------
 // Perf-mode RNG (RT_FLAG_RNG_PHILOX): hipRAND/rocRAND Philox4x32-10 (rocrand_philox4x32_10.h:270-303,
 // rocrand_uniform.h:65-68, 281-284).  The pixel's stream is rocrand_init(seed, subsequence = global
-// pixel index, offset = frame << 34), consumed one block per draw group with rocrand_uniform4: each group
-// of k <= 3 consecutive draws of the reference (camera jitter 2, RandomInUnitSphere attempt 3, dielectric 1)
-// takes the first k words of the stream's next block, philox10(ctr = {g, frame, pixel, 0}, key = seed) for
-// group g of the frame.  A group never spans two blocks, so no word is selected at a lane-varying offset and
-// every group generates exactly one block; nothing per pixel lives in HBM and only the group counter is
-// carried (plus the pixel index); key and frame are launch-uniform kernel arguments.
+// pixel index, offset = frame << 34), consumed in draw groups that start on a block boundary (rocrand_uniform4
+// per block, philox10(ctr = {b, frame, pixel, 0}, key = seed) for the frame's block b): the camera jitter (2
+// draws) and the dielectric's choice (1) take the first words of one block each; a RandomInUnitSphere call takes
+// consecutive words of as many blocks as its attempts need (3 per attempt).  No word is selected at a lane-varying
+// offset; nothing per pixel lives in HBM and only the next block index is carried (plus the pixel index); key and
+// frame are launch-uniform kernel arguments.
 // ---------------------------------------------------------------------------------------------------
 struct RngPhilox {
     uint32_t n, r0, r1, r2, r3, pix;  // n: the next group's block; r0..r3: the current block (not carried)
@@ -824,6 +824,39 @@ __device__ __forceinline__ void draw3(RngPhilox& s, float& a, float& b, float& c
     a = philox_to_uniform(s.r0);
     b = philox_to_uniform(s.r1);
     c = philox_to_uniform(s.r2);
+}
+
+// RandomInUnitSphere (Math.cuh:252-260) in Philox mode: the whole call is one draw group, its attempts taking
+// consecutive words of consecutive blocks (attempt a: words 3a .. 3a + 2 of the call's blocks; four attempts use
+// three blocks, the fourth needs none).  Every lane still looping is at the same attempt, so which words an
+// attempt takes is a wave-uniform branch, not a per-lane select.
+__device__ __forceinline__ f3 random_in_unit_sphere(RngPhilox& s, bool rtl) {
+    f3 p;
+    uint32_t a = 0u;                      // attempt index (the same for every lane in the loop)
+    uint32_t k1 = 0u, k2 = 0u, k3 = 0u;   // words 1-3 of the latest block not drawn yet
+    do {
+        uint32_t x, y, z;
+        const uint32_t phase = a & 3u;
+        if (phase == 0u) {
+            philox_block(s, s.n++);
+            x = s.r0, y = s.r1, z = s.r2, k3 = s.r3;
+        } else if (phase == 1u) {
+            x = k3;
+            philox_block(s, s.n++);
+            y = s.r0, z = s.r1, k2 = s.r2, k3 = s.r3;
+        } else if (phase == 2u) {
+            x = k2, y = k3;
+            philox_block(s, s.n++);
+            z = s.r0, k1 = s.r1, k2 = s.r2, k3 = s.r3;
+        } else {
+            x = k1, y = k2, z = k3;
+        }
+        a++;
+        const float fa = philox_to_uniform(x), fb = philox_to_uniform(y), fc = philox_to_uniform(z);
+        const f3 r = rtl ? mk(fc, fb, fa) : mk(fa, fb, fc);
+        p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
+    } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
+    return p;
 }
 
 __device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPhilox&) {}  // stateless in HBM

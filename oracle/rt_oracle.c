@@ -118,11 +118,11 @@ float orc_curand_uniform(rt_curand_state* s) {
 /* state").  Restates rocRAND's philox4x32_10_engine (/opt/rocm/include/rocrand/                    */
 /* rocrand_philox4x32_10.h:270-303, the Random123 round) and rocrand_uniform (rocrand_uniform.h:    */
 /* 65-68, 281-284).            A pixel's stream is rocrand_init(seed, subsequence = global pixel      */
-/* index, offset = frame << 34), consumed one block per draw group (rocrand_uniform4): each group   */
-/* of k <= 3 consecutive draws of the reference (camera jitter Kernel.cu:139-140, Random()          */
-/* Math.cuh:233, the dielectric's Material.cuh:131) takes the first k words of the next block,      */
-/* philox10(ctr = {g, frame, pixel, 0}, key = {seed lo, seed hi}) for the frame's group g (the      */
-/* kernel's RngPhilox, render.hip).  Pinned by tests/golden/philox_kat.json (rocRAND's own engine). */
+/* index, offset = frame << 34), read as blocks philox10(ctr = {b, frame, pixel, 0}, key = {seed   */
+/* lo, seed hi}) (rocrand_uniform4) in draw groups that start on a block boundary: the camera       */
+/* jitter (Kernel.cu:139-140) and the dielectric's choice (Material.cuh:131) one group each, a      */
+/* whole RandomInUnitSphere call (Math.cuh:252-260, 3 draws per attempt) one group (the kernel's   */
+/* RngPhilox, render.hip).  Pinned by tests/golden/philox_kat.json (rocRAND's own engine).         */
 /* ---------------------------------------------------------------------------------------------- */
 void orc_philox4x32_10(const unsigned int ctr_in[4], const unsigned int key_in[2], unsigned int out[4]) {
     unsigned int c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
@@ -179,8 +179,8 @@ static float orc_uniform(orc_rng* g) {
 /* Random() (Math.cuh:231-234) + RandomInUnitSphere (Math.cuh:252-260). */
 static inline v3 random_in_unit_sphere(orc_rng* st, int order, int* draws) {
     v3 p;
+    orc_group(st); /* Philox: the call's attempts draw consecutive words from a block boundary on */
     do {
-        orc_group(st);
         float a = orc_uniform(st), b = orc_uniform(st), c = orc_uniform(st);
         v3 r = order == 0 ? mk(a, b, c) : mk(c, b, a);
         *draws += 3;
