@@ -231,9 +231,9 @@ enum rt_render_flags {
     RT_FLAG_COUNT_TESTS = 1u << 4, /* also count box and primitive tests into counters[1], [2] */
     RT_FLAG_RNG_PHILOX = 1u << 5,  /* perf-mode RNG: each pixel draws from the hipRAND/rocRAND Philox4x32-10
                                       stream rocrand_init(rng_seed, subsequence = global pixel index,
-                                      offset = rng_frame << 34), one rocrand_uniform4 block per draw group
-                                      (a group of k <= 3 draws — camera jitter, a RandomInUnitSphere attempt,
-                                      the dielectric's choice — takes the block's first k words), instead of
+                                      offset = rng_frame << 34), read as rocrand_uniform4 blocks in draw
+                                      groups that start on a block boundary (the camera jitter, the
+                                      dielectric's choice, a whole RandomInUnitSphere call), instead of
                                       its cuRAND XORWOW state.  `state` is neither read nor written (may be NULL): no
                                       per-pixel RNG bytes in HBM.  Not the reference's stream (its images
                                       match the parity mode statistically, not bit for bit). */
