@@ -226,6 +226,7 @@ struct KParams {
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
+    uint32_t regen_live_frac;        // v3: threshold cap as a fraction of the wave's live pixels (x/64; 0 = off)
 };
 
 constexpr int kStackMax = 64;
@@ -1612,7 +1613,10 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
         if (c.mode == MODE_TRAV) {
-            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt, ntrav);
+            // (RT_TUNE_REGEN_LIVE_FRAC: once pixels finish, the threshold follows the live pixels down)
+            uint32_t thr = threshold;
+            if (P.regen_live_frac) thr = min(thr, ((uint32_t)__popcll(__ballot(c.mode != MODE_DONE)) * P.regen_live_frac) >> 6);
+            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, thr, ro, rd, c, cnt, ntrav);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -2011,6 +2015,10 @@ thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupa
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
+// RT_TUNE_REGEN_LIVE_FRAC: v3's regeneration threshold is capped at 52/64 of the wave's live pixels, so a wave whose
+// pixels are finishing keeps tracing until most of its remaining lanes are done instead of shading a few lanes per
+// leaf pass (C2 −1.0 %, C4 −0.6 %, C3 +0.3 %: profiles/r03o_sweep_regen_live_frac.txt)
+thread_local int g_regen_live_frac = 52;
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
@@ -2251,6 +2259,15 @@ int rt_set_tuning(int key, int value) {
         g_queue_stride = value;
         return prev;
     }
+    if (key == RT_TUNE_REGEN_LIVE_FRAC) {
+        if (value < 0 || value > 64) {
+            set_error("rt_set_tuning: live fraction must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_regen_live_frac;
+        g_regen_live_frac = value;
+        return prev;
+    }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
         if (value < 0 || value > 16) {
             set_error("rt_set_tuning: persistent waves per SIMD must be in [0, 16]");
@@ -2331,6 +2348,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.grid_h = faithful ? (a->height / 16) * 16 : a->height;
     P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
     P.regen_threshold = (uint32_t)g_regen_threshold;
+    P.regen_live_frac = (uint32_t)g_regen_live_frac;
     P.rng_key_lo = (uint32_t)a->rng_seed;
     P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
     P.rng_frame = a->rng_frame;
