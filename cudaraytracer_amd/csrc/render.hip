@@ -2010,15 +2010,18 @@ KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
     }
 }
 
-thread_local int g_regen_threshold = 40;
+// RT_TUNE_REGEN_THRESHOLD: 56 together with the live-pixel cap below (the pair's plateau, 56-64 x 52-60/64, is
+// flat within 0.3 %; 40 without the cap was round 2's optimum: profiles/r03o_sweep_regen_live_frac.txt)
+thread_local int g_regen_threshold = 56;
 thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupancy experiments)
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
-// RT_TUNE_REGEN_LIVE_FRAC: v3's regeneration threshold is capped at 52/64 of the wave's live pixels, so a wave whose
+// RT_TUNE_REGEN_LIVE_FRAC: v3's regeneration threshold is capped at 56/64 of the wave's live pixels, so a wave whose
 // pixels are finishing keeps tracing until most of its remaining lanes are done instead of shading a few lanes per
-// leaf pass (C2 −1.0 %, C4 −0.6 %, C3 +0.3 %: profiles/r03o_sweep_regen_live_frac.txt)
-thread_local int g_regen_live_frac = 52;
+// leaf pass; with it a higher base threshold pays (C2 −2.1 % for the pair against 40 without the cap, C4 −2.4 %,
+// C3 ±0.2 %: profiles/r03o_sweep_regen_live_frac.txt)
+thread_local int g_regen_live_frac = 56;
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread

@@ -302,7 +302,7 @@ int rt_last_variant(void);
 
 /* Tuning knob (per thread); returns the previous value or a negative rt_status.
  *   RT_TUNE_REGEN_THRESHOLD: resumable kernels leave traversal to shade/regenerate finished lanes when
- *   fewer than this many of a wave's 64 lanes are still tracing (1..64, default 40). */
+ *   fewer than this many of a wave's 64 lanes are still tracing (1..64, default 56). */
 /*   RT_TUNE_LEAF_MAX: maximum primitives per BVH leaf used by later rt_scene_create calls (1..4, default 4). */
 /*   RT_TUNE_PERSISTENT_WAVES: waves per SIMD of the persistent kernels' grid (0 = occupancy query, default;
  *   1..16). */
@@ -319,7 +319,7 @@ int rt_last_variant(void);
  *   (a multiple of 64 in [64, 4096], default 64).  RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's 16
  *   queue heads (a power of two in [128, 4096], default 128).  Neither changes the image.
  *   RT_TUNE_REGEN_LIVE_FRAC: the v3 kernels cap the regeneration threshold at this fraction (x/64) of the wave's
- *   pixels still rendering (0 = off; 0..64; default 52).  The image does not depend on it. */
+ *   pixels still rendering (0 = off; 0..64; default 56).  The image does not depend on it. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
