@@ -227,6 +227,7 @@ struct KParams {
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
     uint32_t regen_live_frac;        // v3: threshold cap as a fraction of the wave's live pixels (x/64; 0 = off)
+    uint32_t leaf_break;             // v3: leave the node loop once at most this many lanes still lack a leaf
 };
 
 constexpr int kStackMax = 64;
@@ -1286,7 +1287,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
                                             const float4* __restrict__ nodes_tab, const uint32_t* __restrict__ refs,
                                             const float4* __restrict__ prims, typename RefW<WIDE>::Entry* const stk,
                                             const uint32_t threshold, const f3 ro, const f3 rd, Cursor& c,
-                                            Counts& cnt, const uint32_t ntrav = 64) {
+                                            Counts& cnt, const uint32_t ntrav = 64, const uint32_t leaf_break = 0) {
     // node / leaf references as unsigned values of the reference width (RefW): internal nodes < kSentinel, leaf
     // references (negative in the layout) >= kLeaf; leaf == 0: no postponed leaf
     using RW = RefW<WIDE>;
@@ -1474,7 +1475,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
                       [ch1] "v"(ch1), [t1] "v"(top1), [t2] "v"(top2), [sent] "s"(RW::kSentinel));
                 (void)m0; (void)m2; (void)m3;
                 *sp_entry = (Entry)farc;
-                if (m5 == 0) break;
+                if ((uint32_t)__popcll(m5) <= leaf_break) break;  // (RT_TUNE_LEAF_BREAK)
             }
         }
         const uint64_t t_leaf = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
@@ -1616,7 +1617,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             // (RT_TUNE_REGEN_LIVE_FRAC: once pixels finish, the threshold follows the live pixels down)
             uint32_t thr = threshold;
             if (P.regen_live_frac) thr = min(thr, ((uint32_t)__popcll(__ballot(c.mode != MODE_DONE)) * P.regen_live_frac) >> 6);
-            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, thr, ro, rd, c, cnt, ntrav);
+            v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, thr, ro, rd, c, cnt, ntrav, P.leaf_break);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
@@ -2022,6 +2023,10 @@ thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_
 // leaf pass; with it a higher base threshold pays (C2 −2.1 % for the pair against 40 without the cap, C4 −2.4 %,
 // C3 ±0.2 %: profiles/r03o_sweep_regen_live_frac.txt)
 thread_local int g_regen_live_frac = 56;
+// RT_TUNE_LEAF_BREAK: leave the node loop for the leaf tests once at most 3 traversing lanes still lack a leaf
+// (with the threshold pair above: C2 −2.4 %, C4 −3.5 %, C3 ±0; round 2 measured −1.2 / +1 % at 2 with threshold 40
+// and no cap: profiles/r03r_ab_leaf_break.txt)
+thread_local int g_leaf_break = 3;
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
@@ -2271,6 +2276,15 @@ int rt_set_tuning(int key, int value) {
         g_regen_live_frac = value;
         return prev;
     }
+    if (key == RT_TUNE_LEAF_BREAK) {
+        if (value < 0 || value > 64) {
+            set_error("rt_set_tuning: leaf break must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_leaf_break;
+        g_leaf_break = value;
+        return prev;
+    }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
         if (value < 0 || value > 16) {
             set_error("rt_set_tuning: persistent waves per SIMD must be in [0, 16]");
@@ -2352,6 +2366,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.rius_rtl = (a->flags & RT_FLAG_RIUS_LEFT_TO_RIGHT) ? 0u : 1u;
     P.regen_threshold = (uint32_t)g_regen_threshold;
     P.regen_live_frac = (uint32_t)g_regen_live_frac;
+    P.leaf_break = (uint32_t)g_leaf_break;
     P.rng_key_lo = (uint32_t)a->rng_seed;
     P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
     P.rng_frame = a->rng_frame;
