@@ -2018,11 +2018,12 @@ thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupa
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
-// RT_TUNE_REGEN_LIVE_FRAC: v3's regeneration threshold is capped at 56/64 of the wave's live pixels, so a wave whose
+// RT_TUNE_REGEN_LIVE_FRAC: v3's regeneration threshold is capped at 48/64 of the wave's live pixels, so a wave whose
 // pixels are finishing keeps tracing until most of its remaining lanes are done instead of shading a few lanes per
 // leaf pass; with it a higher base threshold pays (C2 −2.1 % for the pair against 40 without the cap, C4 −2.4 %,
-// C3 ±0.2 %: profiles/r03o_sweep_regen_live_frac.txt)
-thread_local int g_regen_live_frac = 56;
+// C3 ±0.2 %: profiles/r03o_sweep_regen_live_frac.txt; 48 rather than 56 once the leaf-break rule is on, −0.6 %:
+// profiles/r03s_ab_node_min_cap.txt)
+thread_local int g_regen_live_frac = 48;
 // RT_TUNE_LEAF_BREAK: leave the node loop for the leaf tests once at most 3 traversing lanes still lack a leaf
 // (with the threshold pair above: C2 −2.4 %, C4 −3.5 %, C3 ±0; round 2 measured −1.2 / +1 % at 2 with threshold 40
 // and no cap: profiles/r03r_ab_leaf_break.txt)

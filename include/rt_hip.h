@@ -319,7 +319,7 @@ int rt_last_variant(void);
  *   (a multiple of 64 in [64, 4096], default 64).  RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's 16
  *   queue heads (a power of two in [128, 4096], default 128).  Neither changes the image.
  *   RT_TUNE_REGEN_LIVE_FRAC: the v3 kernels cap the regeneration threshold at this fraction (x/64) of the wave's
- *   pixels still rendering (0 = off; 0..64; default 56).  The image does not depend on it.
+ *   pixels still rendering (0 = off; 0..64; default 48).  The image does not depend on it.
  *   RT_TUNE_LEAF_BREAK: the v3 kernels leave the node-visit loop for the leaf tests once at most this many of
  *   the still-traversing lanes hold no leaf (0..64, default 3; 0 = once every lane holds one).  Nor does this. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
