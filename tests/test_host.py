@@ -208,3 +208,17 @@ def test_reference_graph_rejects_non_bvh_world():
     nh, nm, ni = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
     assert lib().rt_reference_graph_flatten(C.addressof(bad), None, C.byref(nh), None, C.byref(nm), None,
                                             C.byref(ni)) == -2
+
+
+def test_scheduling_knobs_defaults_and_ranges():
+    """rt_set_tuning for the v3 scheduling knobs (CPU: no kernel runs): round-3 defaults, range checks, and the
+    previous value returned (include/rt_hip.h rt_tuning_key)."""
+    L = lib()
+    for key, default, bad in [(abi.RT_TUNE_REGEN_THRESHOLD, 56, [0, 65]), (abi.RT_TUNE_REGEN_LIVE_FRAC, 48, [-1, 65]),
+                              (abi.RT_TUNE_LEAF_BREAK, 3, [-1, 65])]:
+        prev = L.rt_set_tuning(key, 7)
+        assert prev == default, (key, prev)
+        assert L.rt_set_tuning(key, prev) == 7
+        for b in bad:
+            assert abi.STATUS.get(L.rt_set_tuning(key, b)) == "RT_ERR_INVALID_ARGUMENT", (key, b)
+        assert L.rt_set_tuning(key, default) == default  # unchanged by the refused values
