@@ -61,6 +61,9 @@ static void free_device(DeviceScene* s) {
     if (s->refs) (void)hipFree((void*)s->refs);
     s->nodes48 = s->refs = nullptr;
     if (s->prims) (void)hipFree((void*)s->prims);
+    if (s->prims_flat) (void)hipFree((void*)s->prims_flat);
+    if (s->ref_nodes) (void)hipFree((void*)s->ref_nodes);
+    s->prims_flat = s->ref_nodes = nullptr;
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);  // texels: owned by rt_scene::texel_block
     s->nodes = s->prims = s->mats = nullptr;
@@ -84,6 +87,10 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.wide_refs = h.wide_refs;
     if ((rc = upload(h.prims, &p, "hipMalloc/hipMemcpy(prims)"))) goto fail;
     d.prims = p;
+    if ((rc = upload(h.prims_flat, &p, "hipMalloc/hipMemcpy(prims_flat)"))) goto fail;
+    d.prims_flat = p;
+    if ((rc = upload(h.ref_nodes, &p, "hipMalloc/hipMemcpy(ref_nodes)"))) goto fail;
+    d.ref_nodes = p;
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
     d.mats = p;
     if ((rc = upload(h.imgs, &p, "hipMalloc/hipMemcpy(images)"))) goto fail;
@@ -101,7 +108,8 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;
-    d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs.size() + h.prims.size() + h.mats.size()) * 4 +
+    d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs.size() + h.prims.size() + h.prims_flat.size() + h.ref_nodes.size() +
+                      h.mats.size()) * 4 +
                      h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;

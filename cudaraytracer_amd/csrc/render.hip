@@ -180,6 +180,23 @@ __device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
     return p;
 }
 
+// The same call resumable (v3, RT_TUNE_RIUS_TRIPS): at most `cap` attempts now; false when every one of them was
+// rejected, and the lane resumes the call at the wave's next shading pass (its RNG state advanced by exactly the
+// attempts made, so the draws, and the accepted point, are those of the uninterrupted loop).  A wave otherwise runs
+// the loop as long as its unluckiest lane: ~4.5 trips for ~1.9 attempts per lane (acceptance π/6).
+__device__ __forceinline__ bool random_in_unit_sphere_capped(Rng& s, bool rtl, uint32_t cap, f3& p) {
+    uint32_t n = 0u;
+    bool inside;
+    do {
+        float a, b, c;
+        draw3(s, a, b, c);
+        const f3 r = rtl ? mk(c, b, a) : mk(a, b, c);
+        p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
+        inside = p.x * p.x + p.y * p.y + p.z * p.z < 1.0f;
+    } while (!inside && ++n < cap);
+    return inside;
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Kernel parameters (by value; everything launch-uniform precomputed on the host with the same
 // binary32 operations the reference performs per thread).
@@ -228,6 +245,8 @@ struct KParams {
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
     uint32_t regen_live_frac;        // v3: threshold cap as a fraction of the wave's live pixels (x/64; 0 = off)
     uint32_t leaf_break;             // v3: leave the node loop once at most this many lanes still lack a leaf
+    uint32_t rius_cap;               // v3: RandomInUnitSphere attempts per shading pass (0xffffffff = unbounded)
+    const float4* ref_nodes;         // flat kernel: the reference BVH over the flat table (ref_trace)
 };
 
 constexpr int kStackMax = 64;
@@ -241,7 +260,7 @@ constexpr uint32_t kQueueAllDone = kQueueCounters == 32 ? 0xffffffffu : (1u << k
 
 // Traversal stack of each kernel family: per-lane scratch array (v1, any scene), 32-bit LDS entries
 // (v2, 32-bit references), 16-bit LDS entries (v3/v4, scenes whose references fit 16 bits)
-enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_LDS16 = 3 };
+enum StackKind { STACK_SCRATCH = 0, STACK_LDS = 1, STACK_LDS16 = 3, STACK_NONE = 4 };
 
 // Per-lane traversal stack of the v1 kernel (the fallback for scenes the LDS kernels cannot hold)
 struct ScratchStack {
@@ -497,8 +516,10 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 // emission, or Scatter of the hit material.  Returns SHADE_ENDED when the path ended (contribution in
 // `contrib`, `emitted * cur_attenuation` or `cur_attenuation * sky`), SHADE_CONTINUE when it continues with
 // (ro, rd, att).
-enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1 };
-template <bool TEX = true, class PP, class R>
+// DEFER (v3): RandomInUnitSphere makes at most P->rius_cap attempts; SHADE_DEFERRED when all were rejected — ro, rd
+// and att are untouched, and the lane shades the same hit again at the next pass, continuing the same call.
+enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1, SHADE_DEFERRED = 2 };
+template <bool TEX = true, bool DEFER = false, class PP, class R>
 __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
                                      f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
@@ -603,7 +624,12 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         ro = p;
         return SHADE_CONTINUE;
     }
-    const f3 q = random_in_unit_sphere(rng, rtl);
+    f3 q;
+    if constexpr (DEFER) {
+        if (!random_in_unit_sphere_capped(rng, rtl, P->rius_cap, q)) return SHADE_DEFERRED;
+    } else {
+        q = random_in_unit_sphere(rng, rtl);
+    }
     const float4 m1 = P->mats[3 * mat + 1];
     f3 attenuation;
     bool ok = true;
@@ -859,6 +885,39 @@ __device__ __forceinline__ f3 random_in_unit_sphere(RngPhilox& s, bool rtl) {
         p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
     } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
     return p;
+}
+
+// Resumable form (RT_TUNE_RIUS_TRIPS): the cap is rounded up to whole four-attempt rounds, so a deferred call
+// stops on a block boundary and resumes at attempt phase 0 with nothing but the block index carried.
+__device__ __forceinline__ bool random_in_unit_sphere_capped(RngPhilox& s, bool rtl, uint32_t cap, f3& p) {
+    cap = cap > 0xfffffff0u ? cap : (cap + 3u) & ~3u;
+    uint32_t a = 0u;
+    uint32_t k1 = 0u, k2 = 0u, k3 = 0u;
+    bool inside;
+    do {
+        uint32_t x, y, z;
+        const uint32_t phase = a & 3u;
+        if (phase == 0u) {
+            philox_block(s, s.n++);
+            x = s.r0, y = s.r1, z = s.r2, k3 = s.r3;
+        } else if (phase == 1u) {
+            x = k3;
+            philox_block(s, s.n++);
+            y = s.r0, z = s.r1, k2 = s.r2, k3 = s.r3;
+        } else if (phase == 2u) {
+            x = k2, y = k3;
+            philox_block(s, s.n++);
+            z = s.r0, k1 = s.r1, k2 = s.r2, k3 = s.r3;
+        } else {
+            x = k1, y = k2, z = k3;
+        }
+        a++;
+        const float fa = philox_to_uniform(x), fb = philox_to_uniform(y), fc = philox_to_uniform(z);
+        const f3 r = rtl ? mk(fc, fb, fa) : mk(fa, fb, fc);
+        p = mk(__builtin_fmaf(2.0f, r.x, -1.0f), __builtin_fmaf(2.0f, r.y, -1.0f), __builtin_fmaf(2.0f, r.z, -1.0f));
+        inside = p.x * p.x + p.y * p.y + p.z * p.z < 1.0f;
+    } while (!inside && a < cap);
+    return inside;
 }
 
 __device__ __forceinline__ void store_rng(const KParams&, uint32_t*, const RngPhilox&) {}  // stateless in HBM
@@ -1613,10 +1672,14 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     while (true) {
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
+        // lanes whose RandomInUnitSphere call was deferred (RT_TUNE_RIUS_TRIPS) wait for the next pass like lanes
+        // whose ray is done; the threshold drops by their number, so a pass still collects as many new hits
+        const uint32_t deferred = (uint32_t)__popcll(__ballot(c.mode == MODE_SHADE));
         if (c.mode == MODE_TRAV) {
             // (RT_TUNE_REGEN_LIVE_FRAC: once pixels finish, the threshold follows the live pixels down)
             uint32_t thr = threshold;
             if (P.regen_live_frac) thr = min(thr, ((uint32_t)__popcll(__ballot(c.mode != MODE_DONE)) * P.regen_live_frac) >> 6);
+            thr = thr > deferred + 1u ? thr - deferred : 1u;
             v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, thr, ro, rd, c, cnt, ntrav, P.leaf_break);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
@@ -1628,12 +1691,15 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             v3_unpark<COMPACT, false>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
-            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+            const int res = shade<TEX, true>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib);
+            bool ended = res == SHADE_ENDED;
+            if (res == SHADE_CONTINUE && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
-            if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
+            if (res == SHADE_DEFERRED) {
+                // (RandomInUnitSphere resumes at the next pass: the lane stays in MODE_SHADE, its ray and hit kept)
+            } else if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
                 col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
                          __uint_as_float(park[(PK_COL + 2) * 64]));
                 v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
@@ -1697,6 +1763,74 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
     return true;
 }
 
+// The persistent kernels' pixel queue (v4, persistent flat), all fields wave-uniform.  The frame's work indices
+// are split over kQueueCounters heads, each owning a contiguous range; a wave draws chunks from its head with one
+// atomic each and moves on to the next live head when its own is exhausted.  Chunks are P.work_chunk indices while
+// the head had plenty left at this wave's last grab, then 64 (other waves draining the same head make that count
+// stale, so a chunk above 64 can still lengthen the frame's tail: RT_TUNE_QUEUE_CHUNK defaults to 64).
+struct PixelQueue {
+    uint32_t qc;                           // the head the wave draws from
+    uint32_t qtried = 0u;                  // heads found exhausted
+    uint32_t wq_next = 0u, wq_end = 0u;    // the wave's current chunk
+    uint32_t head_left = 0xffffffffu;      // the head's remaining indices as of this wave's last grab from it
+    uint32_t wave_pixels = 0u;             // pixels this wave has taken
+    bool drained = false;                  // the frame's queue is empty
+    uint64_t rt_drained = 0u;              // (wave trace) when it found the queue empty
+    __device__ explicit PixelQueue(uint32_t head) : qc(head) {}
+    // Lanes with `need` take the next work indices of the wave's chunk (ballot + mbcnt rank); start(x, g, pix) runs on
+    // every lane that gets a pixel, and its `need` clears.  A lane still needing one afterwards found the queue empty.
+    template <class F>
+    __device__ __forceinline__ void take(const KParams& P, bool& need, F&& start) {
+        uint64_t needm = __ballot(need);
+        while (needm != 0 && !drained) {
+            if (wq_next >= wq_end) {
+                const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+                uint32_t base = 0u;
+                const uint32_t want = head_left > 4u * P.work_chunk ? P.work_chunk : 64u;
+                if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, want);
+                base = __builtin_amdgcn_readlane(base, leader);
+                const uint32_t idx = qc * P.work_per_counter + base;
+                if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
+                    // mark it in the exhausted-heads word and move to the next live head (so a wave probes a few
+                    // heads at the frame's end, not every one of them)
+                    uint32_t done = 0u;
+                    if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * P.queue_stride, 1u << qc);
+                    done = __builtin_amdgcn_readlane(done, leader) | (1u << qc);
+                    if (done == kQueueAllDone || ++qtried >= kQueueCounters) {
+                        drained = true;
+                        if (P.wave_trace) rt_drained = __builtin_amdgcn_s_memrealtime();
+                        break;
+                    }
+                    const uint32_t live = ~done & kQueueAllDone;        // (nonzero here)
+                    const uint32_t above = live & ~((2u << qc) - 1u);   // live heads after qc
+                    qc = (uint32_t)__builtin_ctz(above ? above : live);
+                    head_left = 0u;  // (unknown: small chunks until the first grab there)
+                    continue;
+                }
+                wq_next = idx;
+                // (a chunk ends at its head's range: a head's range is a multiple of 64, not of work_chunk)
+                wq_end = idx + min(want, P.work_per_counter - base);
+                head_left = P.work_per_counter - base - min(want, P.work_per_counter - base);
+            }
+            const uint32_t avail = wq_end - wq_next;
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+            if (need && rank < avail) {
+                uint32_t x, g, pix;
+                if (work_pixel(P, wq_next + rank, x, g, pix)) {
+                    need = false;
+                    start(x, g, pix);
+                }
+            }
+            const uint32_t taken = min((uint32_t)__popcll(needm), avail);
+            wq_next += taken;
+            const uint64_t still = __ballot(need);
+            wave_pixels += (uint32_t)__popcll(needm & ~still);
+            needm = still;
+        }
+    }
+};
+
 template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false, int WAVES_PER_SIMD = 1>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
@@ -1718,19 +1852,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
     Cursor c{(int)RefW<WIDE>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_NEED};
-    uint32_t wq_next = 0u, wq_end = 0u;  // wave-uniform: the wave's current chunk of work indices
-    bool drained = false;                // wave-uniform: the frame's queue is empty
-    // wave-uniform: the queue head the wave draws from (one of kQueueCounters, each owning a contiguous
-    // range of the frame; a wave moves on to the next head when its own is exhausted) and heads tried
-    uint32_t qc = blockIdx.x % kQueueCounters, qtried = 0u;
-    // wave-uniform: the head's remaining indices as of this wave's last grab from it.  Chunks of work_chunk
-    // indices (fewer atomics, wider spatially coherent runs of pixels) while plenty remain, then 64: the
-    // indices a wave has taken but not started keep only that wave busy once the queue is dry (the frame's tail)
-    uint32_t head_left = 0xffffffffu;
-    uint32_t wave_pixels = 0u;           // wave-uniform: pixels this wave has taken
+    PixelQueue queue(blockIdx.x % kQueueCounters);
     const uint32_t threshold = P.regen_threshold;
     const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
-    uint64_t rt_drained = 0u;
 
     while (true) {
         if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt);
@@ -1763,61 +1887,17 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
         }
         // pixel regeneration: lanes without a pixel take the next work indices
         bool need = fin || c.mode == MODE_NEED;
-        uint64_t needm = __ballot(need);
-        if (needm != 0) {
+        if (__ballot(need) != 0) {
             if (!shading && need) rays = park[PK_RAYS * 64];
-            while (needm != 0 && !drained) {
-                if (wq_next >= wq_end) {
-                    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
-                    uint32_t base = 0u;
-                    const uint32_t want = head_left > 4u * P.work_chunk ? P.work_chunk : 64u;
-                    if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, want);
-                    base = __builtin_amdgcn_readlane(base, leader);
-                    const uint32_t idx = qc * P.work_per_counter + base;
-                    if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
-                        // mark it in the exhausted-heads word and move to the next live head (so a wave
-                        // probes a few heads at the frame's end, not every one of them)
-                        uint32_t done = 0u;
-                        if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * P.queue_stride, 1u << qc);
-                        done = __builtin_amdgcn_readlane(done, leader) | (1u << qc);
-                        if (done == kQueueAllDone || ++qtried >= kQueueCounters) {
-                            drained = true;
-                            if (P.wave_trace) rt_drained = __builtin_amdgcn_s_memrealtime();
-                            break;
-                        }
-                        const uint32_t live = ~done & kQueueAllDone;        // (nonzero here)
-                        const uint32_t above = live & ~((2u << qc) - 1u);   // live heads after qc
-                        qc = (uint32_t)__builtin_ctz(above ? above : live);
-                        head_left = 0u;  // (unknown: small chunks until the first grab there)
-                        continue;
-                    }
-                    wq_next = idx;
-                    // (a chunk ends at its head's range: a head's range is a multiple of 64, not of work_chunk)
-                    wq_end = idx + min(want, P.work_per_counter - base);
-                    head_left = P.work_per_counter - base - min(want, P.work_per_counter - base);
-                }
-                const uint32_t avail = wq_end - wq_next;
-                const uint32_t rank =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
-                if (need && rank < avail) {
-                    uint32_t x, g, pix;
-                    if (work_pixel(P, wq_next + rank, x, g, pix)) {
-                        need = false;
-                        park[PK_X * 64] = x;
-                        park[PK_G * 64] = g;
-                        park[PK_PIX * 64] = pix;
-                        rng = begin_rng<R>(state_at(P, pix), P.state_stride, g * P.width + x);
-                        col = mk(0.0f, 0.0f, 0.0f);
-                        sample = 0u;
-                        cam = true;
-                    }
-                }
-                const uint32_t taken = min((uint32_t)__popcll(needm), avail);
-                wq_next += taken;
-                const uint64_t still = __ballot(need);
-                wave_pixels += (uint32_t)__popcll(needm & ~still);
-                needm = still;
-            }
+            queue.take(P, need, [&](uint32_t x, uint32_t g, uint32_t pix) {
+                park[PK_X * 64] = x;
+                park[PK_G * 64] = g;
+                park[PK_PIX * 64] = pix;
+                rng = begin_rng<R>(state_at(P, pix), P.state_stride, g * P.width + x);
+                col = mk(0.0f, 0.0f, 0.0f);
+                sample = 0u;
+                cam = true;
+            });
             if (need) c.mode = MODE_DONE;
         }
         if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
@@ -1833,13 +1913,386 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     }
     cnt.rays = park[PK_RAYS * 64];
     // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
-    cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;
+    cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;
     if (P.wave_trace && wave_leader()) {  // ramp / steady state / tail of the persistent grid (tools/v4_timeline.py)
         unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
         w[0] = rt_start;
-        w[1] = rt_drained;
+        w[1] = queue.rt_drained;
         w[2] = __builtin_amdgcn_s_memrealtime();
-        w[3] = wave_pixels;
+        w[3] = queue.wave_pixels;
+    }
+    flush_counts<COUNT_TESTS>(P, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Flat kernel (variant 5): scenes of at most RT_TUNE_FLAT_MAX primitives — BASELINE configs 1, 3 and 5 have 3, 8
+// and 5.  Over a handful of primitives a BVH saves few tests and makes the lanes of a wave diverge: different
+// node paths, leaves of different lengths, a stack per lane.  Here every ray tests every primitive, in the order
+// the reference's own BVH tests them (prims_flat, scene_build.cpp), so all lanes of a wave step through the same
+// primitive at the same time: its record is a scalar load whose values are SGPR operands, its type a wave-uniform
+// branch, and there is no traversal state.  A pass traces one ray for every lane that needs one and then shades
+// every lane; the path state stays in registers (nothing to park: no traversal competes for them).
+// RandomInUnitSphere is capped per pass (P.rius_cap): a lane still rejecting resumes the call at the next pass and
+// skips that pass's trace, instead of every lane of the wave waiting for the wave's slowest sampler.  Per lane the
+// rays, RNG draws and arithmetic are those of the other kernels (tests/test_gpu_parity.py runs it on every case).
+// ---------------------------------------------------------------------------------------------------
+// The reference's own closest-hit query, replayed exactly: BVHNode::Hit (Hittable.cuh:387-439) over the tree the
+// BVHNode constructor builds (ref_nodes, scene_build.cpp), with AABB::Hit (AABB.cuh:30-50) on the reference's boxes and
+// its t_max bookkeeping (a node's box is tested against the closest hit as of its push).  Per lane, with a private
+// stack: the flat kernel runs it only for the rare rays whose answer box culling could change (flat_trace).
+constexpr int kRefStack = 16;  // > kRefTreeMaxDepth (rt_internal.h)
+__device__ __forceinline__ bool ref_box(const float4 lo, const float4 hi, const f3 o, const f3 inv, float t_max) {
+    float t_min = kTmin;
+    const float los[3] = {lo.x, lo.y, lo.z}, his[3] = {hi.x, hi.y, hi.z};
+    const float os[3] = {o.x, o.y, o.z}, invs[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        float t0 = (los[a] - os[a]) * invs[a];
+        float t1 = (his[a] - os[a]) * invs[a];
+        if (invs[a] < 0.0f) {
+            const float tmp = t0;
+            t0 = t1;
+            t1 = tmp;
+        }
+        t_min = t0 > t_min ? t0 : t_min;
+        t_max = t1 < t_max ? t1 : t_max;
+        if (t_max <= t_min) return false;
+    }
+    return true;
+}
+struct HitOut {
+    int hit;
+    uint32_t tag;
+    float t;
+};
+// (not inlined: the flat kernels' registers are sized for their common path; the result comes back in registers)
+__device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, const float4* __restrict__ prims, const f3 o,
+                                         const f3 d) {
+    int hit = -1;
+    uint32_t tag = 0u;
+    float t_best = FLT_MAX;  // = rec.t once something is hit (the reference's "hit_something ? rec.t : t_max")
+    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float a_dd = dot(d, d);
+    int stk[kRefStack];
+    float stm[kRefStack];
+    if (!ref_box(rnodes[0], rnodes[1], o, inv, FLT_MAX)) return HitOut{hit, tag, t_best};  // its own box first (:389)
+    int top = 0;
+    stk[0] = 0;
+    stm[0] = FLT_MAX;
+    while (top >= 0) {
+        const int n = stk[top];
+        const float tm = stm[top];
+        top--;
+        const float4 lo = rnodes[2 * n], hi = rnodes[2 * n + 1];
+        if (!ref_box(lo, hi, o, inv, tm)) continue;
+        const int ch[2] = {__float_as_int(lo.w), __float_as_int(hi.w)};
+        for (int k = 0; k < 2; k++) {
+            if (ch[k] >= 0) {
+                top++;
+                stk[top] = ch[k];
+                stm[top] = t_best;
+                continue;
+            }
+            const int i = ~ch[k];  // PerformHit (Hittable.cuh:470-485) with t_max = the closest hit so far
+            const float4 q0 = prims[2 * i], q1 = prims[2 * i + 1];
+            const uint32_t type = __float_as_uint(q1.w) & 15u;
+            if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                const f3 oc = sub(o, xyz(q0));
+                const float b = dot(oc, d);
+                const float c = dot(oc, oc) - q1.x;
+                const float disc = b * b - a_dd * c;
+                if (disc > 0) {
+                    float t = (-b - sqrtf(disc)) / a_dd;
+                    if (!(t < t_best && t > kTmin)) t = (-b + sqrtf(disc)) / a_dd;
+                    if (t < t_best && t > kTmin) {
+                        t_best = t;
+                        hit = i;
+                        tag = __float_as_uint(q1.w);
+                    }
+                }
+            } else {  // XY/XZ/YZRect::Hit
+                const float ok = type == RT_XYRECT ? o.z : (type == RT_XZRECT ? o.y : o.x);
+                const float ik = type == RT_XYRECT ? inv.z : (type == RT_XZRECT ? inv.y : inv.x);
+                const float t = (q0.x - ok) * ik;
+                if (!(t < kTmin || t > t_best)) {
+                    const float oa = type == RT_YZRECT ? o.y : o.x, da = type == RT_YZRECT ? d.y : d.x;
+                    const float ob = type == RT_XYRECT ? o.y : o.z, db = type == RT_XYRECT ? d.y : d.z;
+                    const float xx = oa + t * da;
+                    const float yy = ob + t * db;
+                    if (!(xx < q0.y || xx > q0.z || yy < q0.w || yy > q1.x)) {
+                        t_best = t;
+                        hit = i;
+                        tag = __float_as_uint(q1.w);
+                    }
+                }
+            }
+        }
+    }
+    return HitOut{hit, tag, t_best};
+}
+
+// Closest hit over all n primitives of the flat table (PerformHit, Hittable.cuh:470-485, for each in turn), then
+// whether the reference's box culling could have answered differently.  Without culling the query returns the
+// geometric closest hit p* at t*; the reference returns it too unless (a) a box on p*'s path rejects the ray — its
+// boxes contain p*'s own (SurroundingBox), so only if p*'s hit point lies on or within rounding of a face of p*'s own
+// box: within 2^-18 relative of a face in the axes where t* and the box test compute differently, or a slab distance
+// of the rect's own plane axis equal to t* (both are (plane - o) · (1/d), monotone in the plane), — or (b) another
+// primitive ties with t* (which one the reference keeps depends on its culling and order), or (c) a NaN took part.
+// Those rays (about 1e-5 of them) replay the reference exactly (ref_trace); the rest are exact as they stand.
+template <bool COUNT_TESTS>
+__device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, const float4* __restrict__ rnodes,
+                                           const uint32_t n, const f3 ro, const f3 rd, int& hit, uint32_t& tag,
+                                           float& t_best, Counts& cnt) {
+    hit = -1;
+    tag = 0u;
+    t_best = FLT_MAX;
+    bool tie = false, nan = false;  // a candidate equal to the closest hit so far / an accepted NaN distance
+    const float a_dd = dot(rd, rd);
+    const bool fast_div = a_dd >= 0x1p-40f && a_dd <= 0x1p40f;  // RN(1/a) for the sphere roots (div_rn)
+    const float inv_a = rcp_rn(a_dd);
+    // 1.0f / d of each axis (the rect tests' inv_d*, Hittable.cuh:149), once per ray instead of once per rect
+    const float ix = rcp_ieee(rd.x), iy = rcp_ieee(rd.y), iz = rcp_ieee(rd.z);
+    // XY/XZ/YZRect::Hit (Hittable.cuh:140-169, 196-225, 252-281) with the plane axis k and in-plane axes a, b
+    const auto rect = [&](const float4 q0, const float4 q1, const uint32_t i, const float ok, const float ik,
+                          const float oa, const float da, const float ob, const float db) {
+        const float t = (q0.x - ok) * ik;
+        if (!(t < kTmin || t > t_best)) {
+            const float xx = oa + t * da;
+            const float yy = ob + t * db;
+            if (!(xx < q0.y || xx > q0.z || yy < q0.w || yy > q1.x)) {
+                tie = t == t_best;
+                nan |= t != t;
+                t_best = t;
+                hit = (int)i;
+                tag = __float_as_uint(q1.w);
+            }
+        }
+    };
+    for (uint32_t i = 0; i < n; i++) {
+        // wave-uniform record: scalar loads through the constant cache
+        const ConstF32* q = (const ConstF32*)((const ConstU8*)prims + i * 32u);
+        const float4 q0 = make_float4(q[0], q[1], q[2], q[3]), q1 = make_float4(q[4], q[5], q[6], q[7]);
+        const uint32_t type = __float_as_uint(q1.w) & 15u;
+        if (COUNT_TESTS) cnt.prims++;
+        if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+            const f3 oc = sub(ro, xyz(q0));
+            const float b = dot(oc, rd);
+            const float c = dot(oc, oc) - q1.x;
+            const float disc = b * b - a_dd * c;
+            if (disc > 0) {
+                const float sq = sqrt_fast(disc);
+                float t = fast_div ? div_rn(-b - sq, a_dd, inv_a) : (-b - sq) / a_dd;
+                tie |= t == t_best;
+                if (!(t < t_best && t > kTmin)) {
+                    t = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
+                    tie |= t == t_best;
+                }
+                if (t < t_best && t > kTmin) {
+                    tie = false;
+                    t_best = t;
+                    hit = (int)i;
+                    tag = __float_as_uint(q1.w);
+                }
+            }
+        } else if (type == RT_XYRECT) {
+            rect(q0, q1, i, ro.z, iz, ro.x, rd.x, ro.y, rd.y);
+        } else if (type == RT_XZRECT) {
+            rect(q0, q1, i, ro.y, iy, ro.x, rd.x, ro.z, rd.z);
+        } else {  // YZRect: y from the height, z from the width (Hittable.cuh:255-258)
+            rect(q0, q1, i, ro.x, ix, ro.y, rd.y, ro.z, rd.z);
+        }
+    }
+    // (a): p*'s hit point against the faces of p*'s own reference box
+    bool edge = false;
+    if (hit >= 0) {
+        const float4 q0 = prims[2 * hit], q1 = prims[2 * hit + 1];
+        const uint32_t type = tag & 15u;
+        const float ps[3] = {ro.x + t_best * rd.x, ro.y + t_best * rd.y, ro.z + t_best * rd.z};
+        const float os[3] = {ro.x, ro.y, ro.z}, ds[3] = {rd.x, rd.y, rd.z}, is[3] = {ix, iy, iz};
+        const int k = type == RT_SPHERE ? -1 : (type == RT_XYRECT ? 2 : (type == RT_XZRECT ? 1 : 0));
+        const int ia = k == 0 ? 1 : 0;  // the rect's first in-plane axis (a0, a1; the other holds b0, b1)
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            float lo, hi;
+            if (k < 0) {
+                lo = q0.x - q0.w;  // (component a below)
+                hi = q0.x + q0.w;
+                if (a == 1) lo = q0.y - q0.w, hi = q0.y + q0.w;
+                if (a == 2) lo = q0.z - q0.w, hi = q0.z + q0.w;
+            } else if (a == k) {
+                // the plane axis: the slab distances (k -/+ 0.0001 - o) · (1/d) bracket t* = (k - o) · (1/d)
+                const float e0 = ((q0.x - 0.0001f) - os[a]) * is[a], e1 = ((q0.x + 0.0001f) - os[a]) * is[a];
+                edge |= e0 == t_best || e1 == t_best;
+                continue;
+            } else {
+                lo = a == ia ? q0.y : q0.w;
+                hi = a == ia ? q0.z : q1.x;
+            }
+            const float slack = 0x1p-18f * (fabsf(os[a]) + fabsf(t_best * ds[a]) + fabsf(lo) + fabsf(hi)) + 0x1p-120f;
+            edge |= fabsf(ps[a] - lo) <= slack || fabsf(ps[a] - hi) <= slack;
+        }
+    }
+    if (tie || nan || edge || t_best != t_best) {
+        const HitOut r = ref_trace(rnodes, prims, ro, rd);
+        hit = r.hit;
+        tag = r.tag;
+        t_best = r.t;
+    }
+}
+
+template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const KParams P) {
+    using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    const float4* __restrict__ prims = P.prims;  // the flat table (rt_render)
+    uint32_t x, g;
+    size_t pix;
+    const uint32_t slot = blockIdx.x;
+    const uint32_t tile = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
+    if (!lane_pixel<64>(P, x, g, pix, tile)) return;
+    const bool rtl = P.rius_rtl != 0;
+    uint32_t* st = state_at(P, pix);
+    R rng = begin_rng<R>(st, P.state_stride, g * P.width + x);  // global pixel index (Kernel.cu:119)
+
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    f3 col = mk(0.0f, 0.0f, 0.0f), att = mk(1.0f, 1.0f, 1.0f);
+    f3 ro = col, rd = col;
+    // (sample = -1: next_sample starts sample 0)
+    uint32_t sample = P.spp > 0 ? (uint32_t)-1 : 0u, depth = 0u, rays = 0u;
+    int mode = MODE_DONE;
+    // A path ended with `contrib` (Kernel.cu:147): the next sample's camera ray (Kernel.cu:139-146), or done.  With
+    // max_depth = 0 every sample is black but still draws its camera jitter (Kernel.cu:79).
+    const auto next_sample = [&](const f3 contrib) {
+        col = add(col, contrib);
+        KParamsC* q = kparams_reload();
+        const Camera cam = lane_camera(q, x, g);
+        while (++sample < P.spp) {
+            camera_ray(q, cam, rng, ro, rd);
+            att = mk(1.0f, 1.0f, 1.0f);
+            depth = 0u;
+            if (P.max_depth > 0u) {
+                mode = MODE_TRAV;
+                return;
+            }
+            col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+        }
+        mode = MODE_DONE;
+    };
+    if (P.spp > 0) next_sample(mk(0.0f, 0.0f, 0.0f));  // (col + 0 = +0)
+
+    const uint64_t w_start = __builtin_amdgcn_s_memtime();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+    int hit = -1;
+    uint32_t tag = 0u;
+    float t = FLT_MAX;
+    while (__ballot(mode != MODE_DONE) != 0) {
+        if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
+            rays++;
+            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.num_prims, ro, rd, hit, tag, t, cnt);
+            mode = MODE_SHADE;
+        }
+        if (mode == MODE_SHADE) {
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            f3 contrib;
+            const int res = shade<TEX, true>(kparams_reload(), prims, hit, tag, t, ro, rd, att, rng, rtl, contrib);
+            if (res == SHADE_ENDED) {
+                next_sample(contrib);
+            } else if (res == SHADE_CONTINUE) {
+                if (++depth >= P.max_depth) next_sample(mk(0.0f, 0.0f, 0.0f));  // Kernel.cu:79
+                else mode = MODE_TRAV;
+            }
+        }
+    }
+    if (P.wave_trace && wave_leader()) {
+        P.wave_trace[2 * tile] = rt_start;
+        P.wave_trace[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (P.tile_cost && wave_leader()) {  // this tile's cost for the next launch's longest-first order
+        const uint64_t c = (__builtin_amdgcn_s_memtime() - w_start) >> 8;
+        P.tile_cost[tile] = c > 0xffffffffull ? 0xffffffffu : (uint32_t)c;
+    }
+    cnt.rays = rays;
+    cnt.primary = P.spp;
+    finish_pixel<COUNT_TESTS>(P, pix, st, rng, col, cnt);
+}
+
+// Persistent flat kernel (variant 6): the flat kernel's closest-hit query in v4's persistent grid — a device-filling
+// grid whose lanes take the next pixel from the frame's work queue as soon as theirs is done (PixelQueue), for frames
+// with few samples per pixel (BASELINE config 5: 1 spp), where a tile wave would idle on its slowest pixels.  The path
+// state stays in registers (no traversal, nothing to park).  Requires spp >= 1 and max_depth >= 1 (rt_render).
+template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD>
+__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persistent(const KParams P) {
+    using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    const float4* __restrict__ prims = P.prims;  // the flat table (rt_render)
+    const bool rtl = P.rius_rtl != 0;
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    R rng{};
+    f3 col = mk(0.0f, 0.0f, 0.0f), att = col, ro = col, rd = col;
+    uint32_t x = 0u, g = 0u, pix = 0u, sample = 0u, depth = 0u, rays = 0u;
+    int mode = MODE_NEED;
+    int hit = -1;
+    uint32_t tag = 0u;
+    float t = FLT_MAX;
+    PixelQueue queue(blockIdx.x % kQueueCounters);
+    const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+    while (true) {
+        if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
+            rays++;
+            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.num_prims, ro, rd, hit, tag, t, cnt);
+            mode = MODE_SHADE;
+        }
+        bool cam = false;
+        if (mode == MODE_SHADE) {
+            if (COUNT_TESTS) cnt.wshade += wave_leader();
+            f3 contrib;
+            const int res = shade<TEX, true>(kparams_reload(), prims, hit, tag, t, ro, rd, att, rng, rtl, contrib);
+            bool ended = res == SHADE_ENDED;
+            if (res == SHADE_CONTINUE && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+                ended = true;
+                contrib = mk(0.0f, 0.0f, 0.0f);
+            }
+            if (ended) {
+                col = add(col, contrib);  // Kernel.cu:147
+                if (++sample < P.spp) {
+                    cam = true;
+                } else {  // the pixel is done (Kernel.cu:149-157)
+                    write_pixel(P, pix, state_at(P, pix), rng, col);
+                    mode = MODE_NEED;
+                }
+            } else if (res == SHADE_CONTINUE) {
+                mode = MODE_TRAV;
+            }
+        }
+        // pixel regeneration: lanes without a pixel take the next work indices
+        bool need = mode == MODE_NEED;
+        if (__ballot(need) != 0) {
+            queue.take(P, need, [&](uint32_t nx, uint32_t ng, uint32_t npix) {
+                x = nx;
+                g = ng;
+                pix = npix;
+                rng = begin_rng<R>(state_at(P, npix), P.state_stride, ng * P.width + nx);  // Kernel.cu:119-123
+                col = mk(0.0f, 0.0f, 0.0f);
+                sample = 0u;
+                cam = true;
+            });
+            if (need) mode = MODE_DONE;
+        }
+        if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
+            KParamsC* q = kparams_reload();
+            camera_ray(q, lane_camera(q, x, g), rng, ro, rd);
+            att = mk(1.0f, 1.0f, 1.0f);
+            depth = 0u;
+            mode = MODE_TRAV;
+        }
+        if (__ballot(mode != MODE_DONE) == 0) break;
+    }
+    cnt.rays = rays;
+    cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
+    if (P.wave_trace && wave_leader()) {  // (tools/v4_timeline.py)
+        unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
+        w[0] = rt_start;
+        w[1] = queue.rt_drained;
+        w[2] = __builtin_amdgcn_s_memrealtime();
+        w[3] = queue.wave_pixels;
     }
     flush_counts<COUNT_TESTS>(P, cnt);
 }
@@ -1954,6 +2407,9 @@ using KernelFn = void (*)(const dev::KParams);
 //   4  v4: persistent work queue, 64-B nodes      — timed against 3 below 64 spp (a compact-parking, 48-B-node,
 //         longest-first-ordered v4 measured slower on C2, C3 and C5: profiles/r02_ab_v3_v4compact_c2.txt,
 //         profiles/r02_configs_v345.txt)
+//   5  flat: no BVH, every primitive per ray        — automatic choice (in 3's place) for scenes of at most
+//         RT_TUNE_FLAT_MAX primitives
+//   6  persistent flat: 5 in v4's persistent grid — in 4's place for those scenes
 struct Variant {
     int stack;        // StackKind
     int lds_depth;    // v2: LDS stack entries per lane
@@ -1963,10 +2419,11 @@ struct Variant {
 };
 constexpr Variant kVariants[] = {
     {dev::STACK_SCRATCH, 0, 256, 1, false}, {dev::STACK_LDS, 24, 64, 2, false}, {dev::STACK_LDS16, 0, 64, 3, false},
-    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false},
+    {dev::STACK_LDS16, 0, 64, 3, true},     {dev::STACK_LDS16, 0, 64, 4, false}, {dev::STACK_NONE, 0, 64, 5, false},
+    {dev::STACK_NONE, 0, 64, 6, false},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
-constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4;
+constexpr int kVarV1 = 0, kVarV2 = 1, kVarV3 = 2, kVarV3Compact = 3, kVarV4 = 4, kVarFlat = 5, kVarFlatPersistent = 6;
 
 template <int W, bool PH = false, bool C = false, bool WD = false>
 KernelFn v3_pick(bool count, bool tex) {
@@ -1989,7 +2446,22 @@ KernelFn v4_pick(bool count, bool tex) {
 constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
 constexpr int kPhiloxCompactWaves = 8;  // ... of the non-texture Philox build of variant 3
 
+constexpr int kFlatWaves = 8;  // __launch_bounds__ waves per SIMD of the untextured flat kernel
+template <bool PH>
+KernelFn flat_pick(bool count, bool tex, bool persistent) {
+    if (persistent) {
+        if (tex)
+            return count ? dev::render_kernel_flat_persistent<true, true, PH, 1> : dev::render_kernel_flat_persistent<false, true, PH, 1>;
+        return count ? dev::render_kernel_flat_persistent<true, false, PH, 1> : dev::render_kernel_flat_persistent<false, false, PH, 1>;
+    }
+    if (tex) return count ? dev::render_kernel_flat<true, true, PH, 1> : dev::render_kernel_flat<false, true, PH, 1>;
+    return count ? dev::render_kernel_flat<true, false, PH, 1> : dev::render_kernel_flat<false, false, PH, kFlatWaves>;
+}
+
 KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
+    if (variant == kVarFlat || variant == kVarFlatPersistent)
+        return philox ? flat_pick<true>(count, tex, variant == kVarFlatPersistent)
+                      : flat_pick<false>(count, tex, variant == kVarFlatPersistent);
     if (wide) {  // 32-bit references: builds of the compact v3 and of v4 only (rt_render maps wide scenes there)
         if (variant == kVarV3Compact)
             return philox ? v3_pick<1, true, true, true>(count, tex) : v3_pick<1, false, true, true>(count, tex);
@@ -2028,6 +2500,13 @@ thread_local int g_regen_live_frac = 48;
 // (with the threshold pair above: C2 −2.4 %, C4 −3.5 %, C3 ±0; round 2 measured −1.2 / +1 % at 2 with threshold 40
 // and no cap: profiles/r03r_ab_leaf_break.txt)
 thread_local int g_leaf_break = 3;
+// RT_TUNE_RIUS_TRIPS: RandomInUnitSphere attempts per v3 shading pass before a rejecting lane defers the rest of the
+// call to the next pass (0 = unbounded)
+thread_local int g_rius_trips = 0;
+// RT_TUNE_FLAT_MAX: scenes of at most this many primitives run the flat kernel (variant 5) where the automatic choice
+// would run v3; RT_TUNE_FLAT_RIUS_TRIPS: its RandomInUnitSphere attempts per pass (0 = unbounded)
+thread_local int g_flat_max = 16;
+thread_local int g_flat_rius_trips = 2;
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
@@ -2286,6 +2765,33 @@ int rt_set_tuning(int key, int value) {
         g_leaf_break = value;
         return prev;
     }
+    if (key == RT_TUNE_RIUS_TRIPS) {
+        if (value < 0 || value > 64) {
+            set_error("rt_set_tuning: RandomInUnitSphere trips must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_rius_trips;
+        g_rius_trips = value;
+        return prev;
+    }
+    if (key == RT_TUNE_FLAT_MAX) {
+        if (value < 0 || value > (int)kFlatMaxPrims) {
+            set_error("rt_set_tuning: flat kernel primitive limit must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_flat_max;
+        g_flat_max = value;
+        return prev;
+    }
+    if (key == RT_TUNE_FLAT_RIUS_TRIPS) {
+        if (value < 0 || value > 64) {
+            set_error("rt_set_tuning: RandomInUnitSphere trips must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_flat_rius_trips;
+        g_flat_rius_trips = value;
+        return prev;
+    }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
         if (value < 0 || value > 16) {
             set_error("rt_set_tuning: persistent waves per SIMD must be in [0, 16]");
@@ -2420,8 +2926,12 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     std::shared_ptr<AutoChoice> trial;  // this frame is timed for the automatic choice: events ev[trial_slot..+1]
     int trial_slot = 0;
     const bool automatic = variant < 0 || variant >= kNumVariants;
+    // small scenes: the flat kernel takes v3's place (in the trial below 64 spp as well)
+    const bool flat_ok = S.prims_flat && S.num_prims <= (uint32_t)g_flat_max;
+    const int tile_kernel = flat_ok ? kVarFlat : kVarV3Compact;
+    const int persistent_kernel = flat_ok ? kVarFlatPersistent : kVarV4;
     if (automatic) {
-        variant = a->samples_per_pixel < 32 ? kVarV4 : kVarV3Compact;
+        variant = a->samples_per_pixel < 32 ? persistent_kernel : tile_kernel;
         if (a->samples_per_pixel > 0 && a->samples_per_pixel < kAutoSpp && a->max_depth > 0) {
             int device = 0;
             (void)hipGetDevice(&device);
@@ -2438,7 +2948,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
             if (ac.chosen >= 0) {
                 variant = ac.chosen;
             } else if (ac.stage < 3) {
-                variant = ac.stage < 2 ? kVarV3Compact : kVarV4;
+                variant = ac.stage < 2 ? tile_kernel : persistent_kernel;
                 if (ac.stage >= 1) {
                     trial_slot = ac.stage == 1 ? 0 : 2;
                     if ((ac.ev[trial_slot] || hipEventCreate(&ac.ev[trial_slot]) == hipSuccess) &&
@@ -2451,7 +2961,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                 float t3 = -1.0f, t4 = -1.0f;
                 (void)hipEventElapsedTime(&t3, ac.ev[0], ac.ev[1]);
                 (void)hipEventElapsedTime(&t4, ac.ev[2], ac.ev[3]);
-                ac.chosen = (t3 >= 0.0f && t4 >= 0.0f && t4 < t3) ? kVarV4 : kVarV3Compact;
+                ac.chosen = (t3 >= 0.0f && t4 >= 0.0f && t4 < t3) ? persistent_kernel : tile_kernel;
                 variant = ac.chosen;
             } else if (!ac.ev[1] || !ac.ev[3]) {
                 ac.chosen = variant;  // no events: keep the static rule
@@ -2461,10 +2971,13 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
     const bool packable =
         a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u;
+    if (variant == kVarFlat && !S.prims_flat) variant = kVarV3Compact;  // (a scene beyond kFlatMaxPrims)
+    if (variant == kVarFlatPersistent && !S.prims_flat) variant = kVarV4;
     if (kVariants[variant].compact && !packable) variant = kVarV3;  // packed counters would overflow
-    if (kVariants[variant].kernel == 4 && (a->samples_per_pixel == 0 || a->max_depth == 0))
-        variant = packable ? kVarV3Compact : kVarV3;  // the persistent kernel assumes every pixel traces a ray
-    if (philox && kVariants[variant].stack != dev::STACK_LDS16)
+    if ((kVariants[variant].kernel == 4 || kVariants[variant].kernel == 6) && (a->samples_per_pixel == 0 || a->max_depth == 0))
+        variant = kVariants[variant].kernel == 6 ? kVarFlat  // the persistent kernels assume every pixel traces a ray
+                                                 : (packable ? kVarV3Compact : kVarV3);
+    if (philox && kVariants[variant].stack != dev::STACK_LDS16 && kVariants[variant].stack != dev::STACK_NONE)
         variant = packable ? kVarV3Compact : kVarV3;  // the v1/v2 kernels have no Philox build
     // Scenes whose references need 32 bits (S.wide_refs: >= 32767 nodes or >= 8192 primitives) run the WIDE builds
     // of the compact v3 and of v4; the 15-word v3 has none: v2 / v1 there (no Philox build either).
@@ -2482,7 +2995,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         }
     }
     const Variant& V = kVariants[variant];
-    const bool persistent = V.kernel == 4;
+    const bool persistent = V.kernel == 4 || V.kernel == 6;
     // near-first traversal holds at most one deferred child per level below the root
     if (V.stack == dev::STACK_LDS && S.depth > (uint32_t)V.lds_depth + 1) {
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
@@ -2503,6 +3016,12 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         return RT_ERR_UNSUPPORTED;
     }
     KernelFn fn = pick(variant, count_tests, S.has_textures, philox, wide);
+    if (V.kernel == 5 || V.kernel == 6) {  // the flat kernels' tables: primitives in the reference's test order, its BVH
+        P.prims = (const float4*)S.prims_flat;
+        P.ref_nodes = (const float4*)S.ref_nodes;
+    }
+    const int trips = V.kernel >= 5 ? g_flat_rius_trips : g_rius_trips;
+    P.rius_cap = trips > 0 ? (uint32_t)trips : 0xffffffffu;
     const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave
     P.tiles_x = (a->width + tile - 1) / tile;
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
@@ -2529,7 +3048,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     }
     P.num_tiles = tiles;
     std::shared_ptr<TilePlan> plan;
-    if (V.kernel == 3 && g_adaptive_order && !g_tile_order) {
+    if ((V.kernel == 3 || V.kernel == 5) && g_adaptive_order && !g_tile_order) {
         int device = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
         if (rc == RT_OK) rc = acquire_plan(PlanKey{device, (void*)s, P.tiles_x, tiles, V.kernel}, s, &plan);

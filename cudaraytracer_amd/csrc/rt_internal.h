@@ -47,6 +47,8 @@ extern thread_local int g_leaf_max;  // rt_set_tuning(RT_TUNE_LEAF_MAX): 1..kLea
 extern thread_local int g_sah_traversal_x10;  // rt_set_tuning(RT_TUNE_SAH_TRAVERSAL): SAH node cost × 10
 extern thread_local int g_texel_bytes;  // rt_set_tuning(RT_TUNE_TEXEL_LAYOUT): device bytes per texel, 3 or 4
 constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) traversal stack
+constexpr uint32_t kFlatMaxPrims = 64;  // scenes up to this many primitives also get the flat kernel's tables
+constexpr uint32_t kRefTreeMaxDepth = 14;  // deepest reference BVH the flat kernel replays (render.hip kRefStack)
 
 struct HostScene {
     std::vector<float> nodes;   // 16 floats per node
@@ -67,6 +69,9 @@ struct HostScene {
     bool has_image_textures = false;
     bool has_textures = false;  // any CHECKER or IMAGE albedo
     std::vector<int32_t> prim_source;  // desc index of each primitive (BVH order)
+    std::vector<float> prims_flat;     // scenes of <= kFlatMaxPrims primitives: the records in the reference BVH's
+                                       // test order (the flat kernel's table), else empty
+    std::vector<float> ref_nodes;      // ... and the reference BVH itself: 8 floats per node (scene_build.cpp)
 };
 
 // Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.  with_texels = false computes

@@ -14,6 +14,8 @@ struct DeviceScene {
     const void* refs = nullptr;    // per node: uint32 of two 16-bit child references, or (wide_refs) two uint32
     bool wide_refs = false;
     const void* prims = nullptr;   // float4 × 2 per primitive
+    const void* prims_flat = nullptr;  // the same records in the reference BVH's test order (small scenes), or NULL
+    const void* ref_nodes = nullptr;   // the reference BVH (boxes + shape) over prims_flat, or NULL
     const void* mats = nullptr;    // float4 × 3 per material
     const void* imgs = nullptr;    // int4 per image
     const void* texels = nullptr;  // RGB8

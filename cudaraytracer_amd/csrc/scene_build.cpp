@@ -207,6 +207,98 @@ struct Builder {
     }
 };
 
+// The 32-B primitive record (rt_internal.h).
+void pack_prim(const rt_hittable_desc& h, float* o) {
+    uint32_t tag = (uint32_t)h.type | ((uint32_t)h.material << 4);
+    if (h.type == RT_SPHERE) {
+        o[0] = h.center[0]; o[1] = h.center[1]; o[2] = h.center[2]; o[3] = h.radius;
+        // o[5]: RN(1/radius) for the kernel's fast normal division (render.hip divs_rn), 0 = IEEE division
+        const float ar = std::fabs(h.radius);
+        o[4] = h.radius * h.radius; o[5] = (ar >= 0x1p-40f && ar <= 0x1p40f) ? 1.0f / h.radius : 0.0f; o[6] = 0.0f;
+    } else {
+        RectGeom g = rect_geom(h);
+        o[0] = g.k; o[1] = g.a0; o[2] = g.a1; o[3] = g.b0;
+        o[4] = g.b1; o[5] = 0.0f; o[6] = 0.0f;
+    }
+    o[7] = bits_to_float(tag);
+}
+
+// The reference BVH over objs[b, e) exactly as the BVHNode constructor builds it (Hittable.cuh:303-385): the range is
+// sorted by type; a span of 1 or 2 becomes a node with primitive children (a span-1 node holds its object twice), a
+// larger span splits at the end of the first type group (or in the middle) into two node children.  Node boxes are
+// the reference's: primitive boxes (Hittable.cuh:112-116, 171-181, 227-237, 283-293, not padded further) merged by
+// SurroundingBox (AABB.cuh:53-62).  Children: >= 0 node index, < 0 ~(desc index).  Returns the node index.
+struct RefNode {
+    float lo[3], hi[3];
+    int child[2];
+    uint32_t depth;
+};
+void ref_prim_box(const rt_hittable_desc& h, float lo[3], float hi[3]) {
+    if (h.type == RT_SPHERE) {
+        for (int i = 0; i < 3; i++) {
+            volatile float c = h.center[i], r = h.radius;
+            lo[i] = c - r;
+            hi[i] = c + r;
+        }
+        return;
+    }
+    RectGeom g = rect_geom(h);
+    lo[g.ia] = g.a0; hi[g.ia] = g.a1;
+    lo[g.ib] = g.b0; hi[g.ib] = g.b1;
+    volatile float k = g.k;
+    lo[g.ik] = k - 0.0001f;
+    hi[g.ik] = k + 0.0001f;
+}
+int build_reference_tree(const rt_hittable_desc* h, std::vector<int>& objs, int b, int e, uint32_t depth,
+                         std::vector<RefNode>* nodes) {
+    const int id = (int)nodes->size();
+    nodes->push_back(RefNode());
+    std::stable_sort(objs.begin() + b, objs.begin() + e, [&](int x, int y) { return h[x].type < h[y].type; });
+    const int span = e - b;
+    int c0, c1;
+    if (span <= 2) {
+        c0 = ~objs[b];
+        c1 = ~objs[span == 1 ? b : b + 1];
+    } else {
+        int mid = b;
+        while (mid < e && h[objs[mid]].type == h[objs[b]].type) mid++;
+        if (mid == b || mid == e) mid = b + span / 2;
+        c0 = build_reference_tree(h, objs, b, mid, depth + 1, nodes);
+        c1 = build_reference_tree(h, objs, mid, e, depth + 1, nodes);
+    }
+    float lo[2][3], hi[2][3];
+    const int ch[2] = {c0, c1};
+    for (int k = 0; k < 2; k++) {
+        if (ch[k] >= 0) {
+            for (int i = 0; i < 3; i++) { lo[k][i] = (*nodes)[ch[k]].lo[i]; hi[k][i] = (*nodes)[ch[k]].hi[i]; }
+        } else {
+            ref_prim_box(h[~ch[k]], lo[k], hi[k]);
+        }
+    }
+    RefNode& n = (*nodes)[id];
+    for (int i = 0; i < 3; i++) {
+        n.lo[i] = std::fmin(lo[0][i], lo[1][i]);
+        n.hi[i] = std::fmax(hi[0][i], hi[1][i]);
+    }
+    n.child[0] = c0;
+    n.child[1] = c1;
+    n.depth = depth;
+    return id;
+}
+
+// BVHNode::Hit (Hittable.cuh:387-439) pops the right child before the left one: the order in which it tests the
+// primitives, box culling aside (culling skips primitives, never reorders them).
+void reference_test_order(const std::vector<RefNode>& nodes, int n, std::vector<int>* out) {
+    const RefNode& r = nodes[n];
+    if (r.child[0] < 0) {
+        out->push_back(~r.child[0]);
+        if (r.child[1] != r.child[0]) out->push_back(~r.child[1]);
+        return;
+    }
+    reference_test_order(nodes, r.child[1], out);
+    reference_test_order(nodes, r.child[0], out);
+}
+
 int check_texture(const rt_texture_desc& t, uint32_t num_images, std::string* err) {
     if (t.type < RT_CONSTANT || t.type > RT_IMAGE) {
         *err = "texture type " + std::to_string(t.type) + " is not CONSTANT/CHECKER/IMAGE";
@@ -447,21 +539,42 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
     out->prims.resize((size_t)out->num_prims * 8);
     out->prim_source.resize(out->num_prims);
     for (uint32_t i = 0; i < out->num_prims; i++) {
-        const rt_hittable_desc& h = desc->hittables[B.prims[B.order[i]].src];
         out->prim_source[i] = B.prims[B.order[i]].src;
-        float* o = out->prims.data() + (size_t)i * 8;
-        uint32_t tag = (uint32_t)h.type | ((uint32_t)h.material << 4);
-        if (h.type == RT_SPHERE) {
-            o[0] = h.center[0]; o[1] = h.center[1]; o[2] = h.center[2]; o[3] = h.radius;
-            // o[5]: RN(1/radius) for the kernel's fast normal division (render.hip divs_rn), 0 = IEEE division
-            const float ar = std::fabs(h.radius);
-            o[4] = h.radius * h.radius; o[5] = (ar >= 0x1p-40f && ar <= 0x1p40f) ? 1.0f / h.radius : 0.0f; o[6] = 0.0f;
-        } else {
-            RectGeom g = rect_geom(h);
-            o[0] = g.k; o[1] = g.a0; o[2] = g.a1; o[3] = g.b0;
-            o[4] = g.b1; o[5] = 0.0f; o[6] = 0.0f;
+        pack_prim(desc->hittables[out->prim_source[i]], out->prims.data() + (size_t)i * 8);
+    }
+    // Small scenes: the primitives once more, in the order the reference's own BVH tests them (the flat kernel,
+    // render.hip, tests every primitive of every ray in this order, so its closest hit breaks exact ties in t as
+    // the reference's does)
+    // together with the reference's own BVH (ref_nodes: its boxes and shape), which the flat kernel replays exactly
+    // for the rare rays whose closest hit lies on a box face or ties (render.hip, ref_trace)
+    if (out->num_prims >= 1 && out->num_prims <= kFlatMaxPrims) {
+        std::vector<int> objs;
+        for (const BuildPrim& p : B.prims) objs.push_back(p.src);
+        std::vector<RefNode> rn;
+        build_reference_tree(desc->hittables, objs, 0, (int)objs.size(), 1, &rn);
+        uint32_t rdepth = 0;
+        for (const RefNode& n : rn) rdepth = std::max(rdepth, n.depth);
+        if (rdepth <= kRefTreeMaxDepth) {
+            std::vector<int> ord;
+            reference_test_order(rn, 0, &ord);
+            std::vector<int> flat_index(desc->num_hittables, -1);
+            out->prims_flat.resize(ord.size() * 8);
+            for (size_t i = 0; i < ord.size(); i++) {
+                flat_index[ord[i]] = (int)i;
+                pack_prim(desc->hittables[ord[i]], out->prims_flat.data() + i * 8);
+            }
+            // per node: (lo.xyz, child 0) (hi.xyz, child 1); a primitive child is ~(its flat index)
+            out->ref_nodes.resize(rn.size() * 8);
+            for (size_t i = 0; i < rn.size(); i++) {
+                float* o = out->ref_nodes.data() + i * 8;
+                for (int k = 0; k < 2; k++) {
+                    const int c = rn[i].child[k];
+                    const int enc = c >= 0 ? c : ~flat_index[~c];
+                    for (int a = 0; a < 3; a++) o[4 * k + a] = k == 0 ? rn[i].lo[a] : rn[i].hi[a];
+                    o[4 * k + 3] = bits_to_float((uint32_t)enc);
+                }
+            }
         }
-        o[7] = bits_to_float(tag);
     }
     return RT_OK;
 }

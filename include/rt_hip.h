@@ -295,7 +295,8 @@ int rt_set_tile_order(const void* order);
  * RNG mode) — both render identical bits — with fallbacks where a kernel's limits are exceeded; 0 = v1
  * (scratch stack, any scene), 1 = v2 (resumable, 32-bit LDS stacks), 2 = v3 (resumable, path state parked in
  * LDS, 16-bit stacks, longest-first tile order), 3 = v3 with compact parking, 4 = v4 (v3 made persistent with
- * a pixel work queue).  Returns the previous value. */
+ * a pixel work queue), 5 = flat (no BVH; scenes of at most 64 primitives, else 3), 6 = flat in the persistent grid
+ * of 4 (else 4).  Returns the previous value. */
 int rt_set_variant(int variant);
 /* The variant the last rt_render on this thread launched (-1 before any). */
 int rt_last_variant(void);
@@ -321,11 +322,20 @@ int rt_last_variant(void);
  *   RT_TUNE_REGEN_LIVE_FRAC: the v3 kernels cap the regeneration threshold at this fraction (x/64) of the wave's
  *   pixels still rendering (0 = off; 0..64; default 48).  The image does not depend on it.
  *   RT_TUNE_LEAF_BREAK: the v3 kernels leave the node-visit loop for the leaf tests once at most this many of
- *   the still-traversing lanes hold no leaf (0..64, default 3; 0 = once every lane holds one).  Nor does this. */
+ *   the still-traversing lanes hold no leaf (0..64, default 3; 0 = once every lane holds one).  Nor does this.
+ *   RT_TUNE_RIUS_TRIPS: the v3 kernels make at most this many RandomInUnitSphere attempts (Math.cuh:252-260) per
+ *   shading pass; a lane whose attempts were all rejected continues the same call at the wave's next pass
+ *   (0 = unbounded; 0..64; Philox mode rounds it up to whole blocks of four attempts).  The draws, and so the
+ *   image, do not depend on it.
+ *   RT_TUNE_FLAT_MAX: scenes of at most this many active primitives (0..64, default 16) run the flat kernel
+ *   (variant 5: no BVH, every ray tests every primitive in the reference BVH's test order) where the automatic
+ *   choice would run variant 3.  RT_TUNE_FLAT_RIUS_TRIPS: RT_TUNE_RIUS_TRIPS for the flat kernel (default 2).
+ *   Neither changes the image. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
-                     RT_TUNE_REGEN_LIVE_FRAC = 9, RT_TUNE_LEAF_BREAK = 10 };
+                     RT_TUNE_REGEN_LIVE_FRAC = 9, RT_TUNE_LEAF_BREAK = 10, RT_TUNE_RIUS_TRIPS = 11,
+                     RT_TUNE_FLAT_MAX = 12, RT_TUNE_FLAT_RIUS_TRIPS = 13 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

@@ -163,7 +163,7 @@ def test_c3_configured_256spp_rows_match_oracle():
                                   st.reshape(cfg.height, cfg.width, -1)[rows, :, :6])
 
 
-@pytest.mark.parametrize("variant", [2, 3, 4])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5])
 def test_image_texture_without_image_is_cyan(variant):
     """RT_IMAGE albedo with image = -1 in a scene with no images: Image::value's data == nullptr branch
     (Texture.cuh:83-84) returns cyan; the kernel must not index the (absent) image table."""

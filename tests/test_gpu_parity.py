@@ -23,9 +23,10 @@ from oracle import py_oracle as po
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = list(range(5))  # every kernel librt_hip.so ships (kVariants in render.hip)
-# v3 (2), v3 compact parking (3), persistent v4 (4)
-KEY_VARIANTS = [2, 3, 4]
+VARIANTS = list(range(7))  # every kernel librt_hip.so ships (kVariants in render.hip)
+# v3 (2), v3 compact parking (3), persistent v4 (4), flat (5: scenes of at most 64 primitives, else 3), persistent
+# flat (6: else 4)
+KEY_VARIANTS = [2, 3, 4, 5, 6]
 
 
 @pytest.fixture(autouse=True)
@@ -437,7 +438,8 @@ def test_20000_sphere_scene_wide_references_match_oracle(variant, rng):
 # ---------------------------------------------------------------------------------------------------
 # Perf-mode RNG (RT_FLAG_RNG_PHILOX): bit-exact with the oracle's Philox restatement, no state buffer
 # ---------------------------------------------------------------------------------------------------
-PHILOX_KERNELS = [-1, 2, 3, 4, 0]  # auto, v3, v3 compact, v4; 0 (v1, no Philox build) maps to v3 compact
+PHILOX_KERNELS = [-1, 2, 3, 4, 0, 5, 6]  # auto, v3, v3 compact, v4, flat, persistent flat; 0 (v1, no Philox build)
+# maps to v3 compact
 
 
 @pytest.mark.parametrize("variant", PHILOX_KERNELS)
@@ -707,8 +709,10 @@ def test_automatic_choice_times_both_kernels_and_keeps_the_bits(config, spp):
         used.append(lib().rt_last_variant())
         torch.cuda.synchronize()
         images.append(r.image().copy())
-    assert used[:3] == [3, 3, 4], used
-    assert used[4:] == [used[4]] * 4 and used[4] in (3, 4), used  # decided by frame 5 (all trials completed)
+    # the flat kernels take v3's and v4's places for small scenes (Cornell: 8 primitives)
+    tile_kernel, persistent = (5, 6) if config == "c3" else (3, 4)
+    assert used[:3] == [tile_kernel, tile_kernel, persistent], used
+    assert used[4:] == [used[4]] * 4 and used[4] in (tile_kernel, persistent), used  # decided by frame 5
     for img in images[1:]:
         np.testing.assert_array_equal(img, images[0])
     lib().rt_set_variant(4)
@@ -718,7 +722,7 @@ def test_automatic_choice_times_both_kernels_and_keeps_the_bits(config, spp):
     assert lib().rt_last_variant() == 4
     lib().rt_set_variant(-1)
     r.render(ds, 64, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_NO_STATE_WRITEBACK)
-    assert lib().rt_last_variant() == 3  # from 64 spp: v3
+    assert lib().rt_last_variant() == tile_kernel  # from 64 spp: v3 (flat for small scenes)
 
 
 @pytest.mark.parametrize("chunk, stride", [(64, 128), (128, 4096), (256, 128), (1024, 4096)])
@@ -743,3 +747,45 @@ def test_persistent_queue_knobs_change_schedule_not_pixels(chunk, stride):
         lib().rt_set_tuning(8, prev_s)
     np.testing.assert_array_equal(r.image(), g["pos"])
     assert int(r.counters[0]) == int(g["counters"][0])
+
+
+# v3 scheduling knobs (rt_hip.h): (key, value) pairs around the defaults, including the extremes
+V3_KNOBS = [(abi.RT_TUNE_RIUS_TRIPS, k) for k in (0, 1, 2, 3, 5)] + \
+           [(abi.RT_TUNE_LEAF_BREAK, k) for k in (0, 1, 64)] + \
+           [(abi.RT_TUNE_REGEN_LIVE_FRAC, k) for k in (0, 1, 64)]
+
+
+@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("key, value", V3_KNOBS, ids=lambda v: str(v))
+def test_v3_scheduling_knobs_change_schedule_not_pixels(key, value, variant):
+    """RT_TUNE_RIUS_TRIPS (a RandomInUnitSphere call split over shading passes), RT_TUNE_LEAF_BREAK and
+    RT_TUNE_REGEN_LIVE_FRAC decide when a v3 wave traverses, tests leaves or shades, never what a lane computes:
+    every setting renders the golden images, ray counts and advanced RNG states (XORWOW) and the Philox goldens."""
+    prev = lib().rt_set_tuning(key, value)
+    assert prev >= 0
+    lib().rt_set_variant(variant)
+    try:
+        for name in ("c2_rtiow_192x112_s16", "c3_cornell_128_s16", "c2_rtiow_ltr_96x64_s8"):
+            case = CASE_BY_NAME[name]
+            cfg, g = case.cfg(), load_golden(case.name)
+            r = Renderer(cfg.width, cfg.height)
+            r.render_init()
+            r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
+            torch.cuda.synchronize()
+            assert lib().rt_last_variant() == variant
+            np.testing.assert_array_equal(r.image(), g["pos"], err_msg=name)
+            assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes(), name
+            assert int(r.counters[0]) == int(g["counters"][0]), name
+        for case, frame in PHILOX_CASES:
+            g = load_golden(f"philox_{case.name}_f{frame}")
+            cfg = case.cfg()
+            r = Renderer(cfg.width, cfg.height, rng="philox")
+            r.render_init(1984)
+            r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags,
+                     frame=frame)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(r.image(), g["pos"], err_msg=f"philox {case.name}")
+            assert int(r.counters[0]) == int(g["counters"][0])
+    finally:
+        lib().rt_set_tuning(key, prev)
+        lib().rt_set_variant(-1)
