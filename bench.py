@@ -11,7 +11,8 @@ kernel itself (one closest-hit query = one iteration of color()'s loop, Kernel.c
       round(1080·√N) (same camera and field of view, ≈2.07 M pixels per GPU), split in block-cyclic 16-row
       bands; every frame is gathered to rank 0 over RCCL on the collective's own stream while the next frame
       renders (parallel.BandGather; the last frame's gather is inside the timed region, gather_ms is the part
-      of it the render stream waited for).
+      of it the render stream waited for).  The line carries other_configs: BASELINE config 4 (the 7680×4320,
+      128 spp frame split over the N ranks + RCCL gather) at every N, and configs 5 and 3 at N = 1.
   --config c3: BASELINE config 3 (3840×2160, 256 spp, depth 16, Cornell box), one GPU.
   --config c4: BASELINE config 4 as configured, strong scaling: one 7680×4320, 128 spp, depth 8 RTIOW frame
       split over the N ranks in 16-row bands (N = 1 renders all of it) + the RCCL gather, whose time is
@@ -123,7 +124,8 @@ def self_launch(args) -> int:
 
 def dry_run(args) -> None:
     """The launch path without a GPU: every rank joins a gloo group and gathers a synthetic band buffer of the
-    configured frame (its global row indices), and rank 0 checks the reassembled frame."""
+    configured frame (its global row indices), and rank 0 checks the reassembled frame; for config 2 the same for
+    config 4's frame (the block other_configs.c4 of a GPU run)."""
     from cudaraytracer_amd.renderer import band_rows_of
     from cudaraytracer_amd import scenes
 
@@ -132,16 +134,27 @@ def dry_run(args) -> None:
         raise SystemExit(f"bench.py --dry-run: WORLD_SIZE={world} but --gpus {args.gpus}")
     if world > 1:
         parallel.init_process_group("gloo")
-    cfg = scenes.CONFIGS[args.config]
-    w, h = 64, cfg.height
-    rows = band_rows_of(h, parallel.DEFAULT_BAND_ROWS, world, rank)
-    local = torch.tensor(rows, dtype=torch.int64).repeat_interleave(w)
-    full = parallel.gather_bands(local, w, h, parallel.DEFAULT_BAND_ROWS) if world > 1 else local.view(h, w)
+
+    def gather_ok(config: str) -> bool | None:
+        cfg = scenes.CONFIGS[config]
+        w, h = 64, cfg.height
+        rows = band_rows_of(h, parallel.DEFAULT_BAND_ROWS, world, rank)
+        local = torch.tensor(rows, dtype=torch.int64).repeat_interleave(w)
+        full = parallel.gather_bands(local, w, h, parallel.DEFAULT_BAND_ROWS) if world > 1 else local.view(h, w)
+        if rank != 0:
+            return None
+        return bool(torch.equal(full, torch.arange(h, dtype=torch.int64)[:, None].expand(h, w)))
+
+    ok = gather_ok(args.config)
+    oc = {"c4": {"frame_ok": gather_ok("c4"), "height": scenes.CONFIGS["c4"].height, "scaling": "strong",
+                 "band_rows": parallel.DEFAULT_BAND_ROWS}} if args.config == "c2" and not args.no_config_lines else None
     if rank == 0:
-        ok = bool(torch.equal(full, torch.arange(h, dtype=torch.int64)[:, None].expand(h, w)))
-        print(json.dumps({"dry_run": True, "world_size": world, "gpus": args.gpus, "config": args.config,
-                          "band_rows": parallel.DEFAULT_BAND_ROWS, "frame_ok": ok}), flush=True)
-        if not ok:
+        line = {"dry_run": True, "world_size": world, "gpus": args.gpus, "config": args.config,
+                "band_rows": parallel.DEFAULT_BAND_ROWS, "frame_ok": ok}
+        if oc is not None:
+            line["other_configs"] = oc
+        print(json.dumps(line), flush=True)
+        if not ok or (oc is not None and not oc["c4"]["frame_ok"]):
             raise SystemExit("bench.py --dry-run: gathered frame differs")
     if world > 1:
         dist.barrier()
@@ -387,6 +400,23 @@ def run_rank(args) -> dict | None:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed, kernel_ms, gather_ms = float(stats[0]), float(stats[1]), float(stats[2])
     rays_all = int(tot[0])
+    gather = None
+    if world > 1:  # one more gather of the last frame, alone and synchronous: the transfer's own time
+        counts = parallel.local_row_counts(cfg.height, band, world)
+        nbytes = (world - 1) * max(counts) * cfg.width * 4  # rank 0 receives every other rank's padded band buffer
+        times = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            dist.barrier()
+            g0 = time.perf_counter()
+            parallel.gather_bands(r.pos, cfg.width, cfg.height, band, reuse=True)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - g0)
+        gs = torch.tensor([min(times)], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(gs, op=dist.ReduceOp.MAX)
+        gather = {"bytes_to_rank0": nbytes, "sync_ms": round(float(gs[0]) * 1e3, 3),
+                  "GBps": round(nbytes / float(gs[0]) / 1e9, 2),
+                  "backend": "RCCL (xGMI)" if args.backend == "nccl" else args.backend}
 
     if rank == 0:
         line = {
@@ -418,6 +448,8 @@ def run_rank(args) -> dict | None:
             "gather_ms": round(gather_ms, 3) if world > 1 else 0.0,
             "rays_per_frame": rays_all // args.steps,
         }
+        if gather is not None:
+            line["gather"] = gather
         if progressive:
             line["roofline"] = hbm_roofline(args, cfg, r, c, kernel_ms)
         else:
@@ -432,8 +464,6 @@ def run_rank(args) -> dict | None:
         if world == 1 and not args.no_cpu_baseline and not strong:
             cpu_inputs = inputs if not progressive else scenes.camera_inputs(*scenes.moving_camera(0, C5_FRAMES), cfg.fov)
             line["cpu_baseline"] = cpu_baseline(cfg, scene_desc, cpu_inputs, args.cpu_seconds)
-    if world > 1:
-        dist.destroy_process_group()
     return line if rank == 0 else None
 
 
@@ -506,6 +536,27 @@ def hbm_roofline(args, cfg, r, c, kernel_ms) -> dict:
     }
 
 
+def other_configs(args, world: int) -> dict | None:
+    """BASELINE configs on the same run's clock beside the C2 headline: config 4 (the 7680x4320, 128 spp frame split
+    over the N ranks in 16-row bands + the RCCL gather) at every N, configs 5 (the real-time progressive path) and 3
+    (Cornell, 256 spp) at N = 1.  Every rank takes part; rank 0 returns the blocks."""
+    out = {}
+    subs = ([("c5", 20, 3), ("c3", 2, 1)] if world == 1 else []) + [("c4", 2, 1)]
+    for name, steps, warmup in subs:
+        sub = argparse.Namespace(**vars(args))
+        sub.config, sub.steps, sub.warmup = name, steps, warmup
+        sub.no_cpu_baseline = sub.no_philox_line = True
+        o = run_rank(sub)
+        if o is not None:
+            out[name] = {k: o[k] for k in ("metric", "value", "unit", "ms_per_step", "kernel_ms", "gather_ms",
+                                           "rays_per_frame", "steps", "warmup", "scaling", "roofline") if k in o}
+            out[name]["workload"] = o["config"]["workload"]
+            out[name]["parallelism"] = o["config"]["parallelism"]
+            if "gather" in o:
+                out[name]["gather"] = o["gather"]
+    return out if parallel.env_rank()[0] == 0 else None
+
+
 def main() -> None:
     args = parse_args()
     launched = "WORLD_SIZE" in os.environ
@@ -519,17 +570,14 @@ def main() -> None:
         run_tiled(args, scenes.CONFIGS[args.config])
         return
     line = run_rank(args)
-    if line is not None and args.config == "c2" and args.gpus == 1 and not args.no_config_lines:
-        # BASELINE configs 5 (the real-time progressive path) and 3 (Cornell, 256 spp) on the same run's clock
-        line["other_configs"] = {}
-        for name, steps, warmup in (("c5", 20, 3), ("c3", 2, 1)):
-            sub = argparse.Namespace(**vars(args))
-            sub.config, sub.steps, sub.warmup = name, steps, warmup
-            sub.no_cpu_baseline = sub.no_philox_line = True
-            o = run_rank(sub)
-            line["other_configs"][name] = {k: o[k] for k in ("metric", "value", "unit", "ms_per_step", "kernel_ms",
-                                                             "rays_per_frame", "steps", "warmup", "roofline")}
-            line["other_configs"][name]["workload"] = o["config"]["workload"]
+    world = parallel.env_rank()[1]
+    if args.config == "c2" and not args.no_config_lines:
+        oc = other_configs(args, world)
+        if line is not None:
+            line["other_configs"] = oc
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
     if line is not None:
         print(json.dumps(line), flush=True)
 

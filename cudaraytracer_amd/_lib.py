@@ -87,7 +87,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_gl_unregister.argtypes = [vp]
     lib.rt_copy_image_to_host.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_int, vp]
     lib.rt_write_ppm.argtypes = [C.c_char_p, vp, C.c_uint32, C.c_uint32, C.c_int]
-    lib.rt_set_wave_trace.argtypes = [C.c_void_p]
+    lib.rt_set_wave_trace.argtypes = [C.c_void_p, C.c_uint64]
     lib.rt_set_tile_order.argtypes = [C.c_void_p]
     lib.rt_last_kernel_ms.restype = C.c_float
     lib.rt_last_variant.restype = C.c_int

@@ -180,7 +180,7 @@ __device__ __forceinline__ f3 random_in_unit_sphere(R& s, bool rtl) {
     return p;
 }
 
-// The same call resumable (v3, RT_TUNE_RIUS_TRIPS): at most `cap` attempts now; false when every one of them was
+// The same call resumable (flat kernels, RT_TUNE_RIUS_TRIPS): at most `cap` attempts now; false when every one of them was
 // rejected, and the lane resumes the call at the wave's next shading pass (its RNG state advanced by exactly the
 // attempts made, so the draws, and the accepted point, are those of the uninterrupted loop).  A wave otherwise runs
 // the loop as long as its unluckiest lane: ~4.5 trips for ~1.9 attempts per lane (acceptance π/6).
@@ -240,12 +240,13 @@ struct KParams {
     uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
     unsigned long long* wave_trace;  // diagnostic: v3 per tile {start, end}; v4 per wave {start, queue drained,
                                      // end, pixels} of s_memrealtime (100 MHz)
+    unsigned long long wave_trace_words;  // its size; a stamp that would not fit is not written
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
     uint32_t regen_live_frac;        // v3: threshold cap as a fraction of the wave's live pixels (x/64; 0 = off)
     uint32_t leaf_break;             // v3: leave the node loop once at most this many lanes still lack a leaf
-    uint32_t rius_cap;               // v3: RandomInUnitSphere attempts per shading pass (0xffffffff = unbounded)
+    uint32_t rius_cap;               // flat: RandomInUnitSphere attempts per shading pass (0xffffffff = unbounded)
     const float4* ref_nodes;         // flat kernel: the reference BVH over the flat table (ref_trace)
 };
 
@@ -516,7 +517,7 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 // emission, or Scatter of the hit material.  Returns SHADE_ENDED when the path ended (contribution in
 // `contrib`, `emitted * cur_attenuation` or `cur_attenuation * sky`), SHADE_CONTINUE when it continues with
 // (ro, rd, att).
-// DEFER (v3): RandomInUnitSphere makes at most P->rius_cap attempts; SHADE_DEFERRED when all were rejected — ro, rd
+// DEFER (flat kernels): RandomInUnitSphere makes at most P->rius_cap attempts; SHADE_DEFERRED when all were rejected — ro, rd
 // and att are untouched, and the lane shades the same hit again at the next pass, continuing the same call.
 enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1, SHADE_DEFERRED = 2 };
 template <bool TEX = true, bool DEFER = false, class PP, class R>
@@ -1672,14 +1673,10 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     while (true) {
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
-        // lanes whose RandomInUnitSphere call was deferred (RT_TUNE_RIUS_TRIPS) wait for the next pass like lanes
-        // whose ray is done; the threshold drops by their number, so a pass still collects as many new hits
-        const uint32_t deferred = (uint32_t)__popcll(__ballot(c.mode == MODE_SHADE));
         if (c.mode == MODE_TRAV) {
             // (RT_TUNE_REGEN_LIVE_FRAC: once pixels finish, the threshold follows the live pixels down)
             uint32_t thr = threshold;
             if (P.regen_live_frac) thr = min(thr, ((uint32_t)__popcll(__ballot(c.mode != MODE_DONE)) * P.regen_live_frac) >> 6);
-            thr = thr > deferred + 1u ? thr - deferred : 1u;
             v3_traverse<COUNT_TESTS, NODES, park_words(COMPACT) * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, thr, ro, rd, c, cnt, ntrav, P.leaf_break);
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
@@ -1691,15 +1688,12 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             v3_unpark<COMPACT, false>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            const int res = shade<TEX, true>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib);
-            bool ended = res == SHADE_ENDED;
-            if (res == SHADE_CONTINUE && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
-            if (res == SHADE_DEFERRED) {
-                // (RandomInUnitSphere resumes at the next pass: the lane stays in MODE_SHADE, its ray and hit kept)
-            } else if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
+            if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
                 col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
                          __uint_as_float(park[(PK_COL + 2) * 64]));
                 v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
@@ -1715,7 +1709,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         if (__ballot(c.mode != MODE_DONE) == 0) break;
     }
     if (COUNT_TESTS) cnt.ctotal = __builtin_amdgcn_s_memtime() - t_start;
-    if (P.wave_trace && wave_leader()) {
+    if (P.wave_trace && wave_leader() && 2ull * tile + 2ull <= P.wave_trace_words) {
         P.wave_trace[2 * tile] = rt_start;
         P.wave_trace[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1914,7 +1908,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     cnt.rays = park[PK_RAYS * 64];
     // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
     cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;
-    if (P.wave_trace && wave_leader()) {  // ramp / steady state / tail of the persistent grid (tools/v4_timeline.py)
+    if (P.wave_trace && wave_leader() && 4ull * blockIdx.x + 4ull <= P.wave_trace_words) {  // (tools/v4_timeline.py)
         unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
         w[0] = rt_start;
         w[1] = queue.rt_drained;
@@ -2052,21 +2046,21 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
     const float inv_a = rcp_rn(a_dd);
     // 1.0f / d of each axis (the rect tests' inv_d*, Hittable.cuh:149), once per ray instead of once per rect
     const float ix = rcp_ieee(rd.x), iy = rcp_ieee(rd.y), iz = rcp_ieee(rd.z);
+    // Both tests branch-free: every lane evaluates the whole test and the closest hit moves by selects (the tests'
+    // results are those of the reference's branches: x and y are pure functions of t, computed whatever t is).
     // XY/XZ/YZRect::Hit (Hittable.cuh:140-169, 196-225, 252-281) with the plane axis k and in-plane axes a, b
     const auto rect = [&](const float4 q0, const float4 q1, const uint32_t i, const float ok, const float ik,
                           const float oa, const float da, const float ob, const float db) {
         const float t = (q0.x - ok) * ik;
-        if (!(t < kTmin || t > t_best)) {
-            const float xx = oa + t * da;
-            const float yy = ob + t * db;
-            if (!(xx < q0.y || xx > q0.z || yy < q0.w || yy > q1.x)) {
-                tie = t == t_best;
-                nan |= t != t;
-                t_best = t;
-                hit = (int)i;
-                tag = __float_as_uint(q1.w);
-            }
-        }
+        const float xx = oa + t * da;
+        const float yy = ob + t * db;
+        // (non-short-circuit & and |: lane-mask arithmetic, no branch)
+        const bool acc = (!(t < kTmin) & !(t > t_best)) & (!(xx < q0.y) & !(xx > q0.z) & !(yy < q0.w) & !(yy > q1.x));
+        tie = (tie & !acc) | (acc & (t == t_best));
+        nan = nan | (acc & (t != t));
+        t_best = acc ? t : t_best;
+        hit = acc ? (int)i : hit;
+        tag = acc ? __float_as_uint(q1.w) : tag;
     };
     for (uint32_t i = 0; i < n; i++) {
         // wave-uniform record: scalar loads through the constant cache
@@ -2079,21 +2073,17 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
             const float b = dot(oc, rd);
             const float c = dot(oc, oc) - q1.x;
             const float disc = b * b - a_dd * c;
-            if (disc > 0) {
-                const float sq = sqrt_fast(disc);
-                float t = fast_div ? div_rn(-b - sq, a_dd, inv_a) : (-b - sq) / a_dd;
-                tie |= t == t_best;
-                if (!(t < t_best && t > kTmin)) {
-                    t = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
-                    tie |= t == t_best;
-                }
-                if (t < t_best && t > kTmin) {
-                    tie = false;
-                    t_best = t;
-                    hit = (int)i;
-                    tag = __float_as_uint(q1.w);
-                }
-            }
+            const bool real = disc > 0;
+            const float sq = sqrt_fast(real ? disc : 1.0f);  // (a dummy argument keeps sqrt_fast's fast path)
+            const float tn = fast_div ? div_rn(-b - sq, a_dd, inv_a) : (-b - sq) / a_dd;
+            const float tf = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
+            const bool near_ok = (tn < t_best) & (tn > kTmin);
+            const float t = near_ok ? tn : tf;  // the far root is tried only when the near one is out of range
+            const bool acc = real & (t < t_best) & (t > kTmin);
+            tie = (tie | (real & ((tn == t_best) | (!near_ok & (tf == t_best))))) & !acc;
+            t_best = acc ? t : t_best;
+            hit = acc ? (int)i : hit;
+            tag = acc ? __float_as_uint(q1.w) : tag;
         } else if (type == RT_XYRECT) {
             rect(q0, q1, i, ro.z, iz, ro.x, rd.x, ro.y, rd.y);
         } else if (type == RT_XZRECT) {
@@ -2202,7 +2192,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
             }
         }
     }
-    if (P.wave_trace && wave_leader()) {
+    if (P.wave_trace && wave_leader() && 2ull * tile + 2ull <= P.wave_trace_words) {
         P.wave_trace[2 * tile] = rt_start;
         P.wave_trace[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -2287,7 +2277,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     }
     cnt.rays = rays;
     cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
-    if (P.wave_trace && wave_leader()) {  // (tools/v4_timeline.py)
+    if (P.wave_trace && wave_leader() && 4ull * blockIdx.x + 4ull <= P.wave_trace_words) {  // (tools/v4_timeline.py)
         unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
         w[0] = rt_start;
         w[1] = queue.rt_drained;
@@ -2488,6 +2478,7 @@ KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
 thread_local int g_regen_threshold = 56;
 thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupancy experiments)
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
+thread_local unsigned long long g_wave_trace_words = 0;
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
 // RT_TUNE_REGEN_LIVE_FRAC: v3's regeneration threshold is capped at 48/64 of the wave's live pixels, so a wave whose
@@ -2500,13 +2491,11 @@ thread_local int g_regen_live_frac = 48;
 // (with the threshold pair above: C2 −2.4 %, C4 −3.5 %, C3 ±0; round 2 measured −1.2 / +1 % at 2 with threshold 40
 // and no cap: profiles/r03r_ab_leaf_break.txt)
 thread_local int g_leaf_break = 3;
-// RT_TUNE_RIUS_TRIPS: RandomInUnitSphere attempts per v3 shading pass before a rejecting lane defers the rest of the
-// call to the next pass (0 = unbounded)
-thread_local int g_rius_trips = 0;
-// RT_TUNE_FLAT_MAX: scenes of at most this many primitives run the flat kernel (variant 5) where the automatic choice
-// would run v3; RT_TUNE_FLAT_RIUS_TRIPS: its RandomInUnitSphere attempts per pass (0 = unbounded)
+// RT_TUNE_FLAT_MAX: scenes of at most this many primitives run the flat kernels (variants 5, 6) where the automatic
+// choice would run v3 / v4.  RT_TUNE_RIUS_TRIPS: their RandomInUnitSphere attempts per pass before a rejecting lane
+// defers the rest of the call to the next pass (0 = unbounded)
 thread_local int g_flat_max = 16;
-thread_local int g_flat_rius_trips = 2;
+thread_local int g_rius_trips = 4;
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
@@ -2596,36 +2585,44 @@ thread_local int g_persistent_waves = 0;  // 0: occupancy query
 constexpr size_t kLdsLimit = 160 * 1024;
 
 // Work-queue heads of the persistent kernel: a ring of counters per device, one slot per launch, zeroed
-// on the launch's stream right before it.  A slot is kQueueBytes (the kQueueCounters heads, up to 4 KB apart,
+// on the launch's stream right before it.  A slot holds the kQueueCounters heads RT_TUNE_QUEUE_STRIDE apart
 // plus the exhausted-heads word) and is reused after kQueueSlots further persistent launches on that device:
 // a caller may keep at most kQueueSlots persistent launches in flight per device (rt_hip.h, rt_render).
 constexpr uint32_t kQueueSlots = 256;
 constexpr uint32_t kQueueMaxStride = 4096;  // bytes between heads (RT_TUNE_QUEUE_STRIDE)
-constexpr uint32_t kQueueBytes = (dev::kQueueCounters + 1u) * kQueueMaxStride;
-thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 queue heads
+thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's queue heads
 thread_local int g_queue_chunk = 64;    // RT_TUNE_QUEUE_CHUNK: work indices per queue atomic
 constexpr int kMaxDevices = 64;
 struct QueueRing {
     uint32_t* buf = nullptr;
+    size_t slot_bytes = 0;  // (kQueueCounters + 1) heads at the largest stride used so far on the device
     std::atomic<uint32_t> next{0};
     int cus = 0;
 };
 QueueRing g_queues[kMaxDevices];
 std::mutex g_queue_mu;
 
-int acquire_queue(int device, uint32_t** head, int* cus) {
+// The next queue slot of `device` for heads `stride` bytes apart.  The ring is sized for the stride in use (2 KB
+// slots at the default 128 B); a larger stride re-allocates it, after the device has drained (hipFree waits).
+int acquire_queue(int device, uint32_t stride, uint32_t** head, int* cus) {
     if (device < 0 || device >= kMaxDevices) {
         set_error("rt_render: device ordinal out of range");
         return RT_ERR_DEVICE;
     }
     QueueRing& q = g_queues[device];
-    {
-        std::lock_guard<std::mutex> lock(g_queue_mu);
-        if (!q.buf) {
-            void* p = nullptr;
-            int rc = hip_check(hipMalloc(&p, (size_t)kQueueSlots * kQueueBytes), "rt_render: work queue allocation");
-            if (rc != RT_OK) return rc;
-            q.buf = (uint32_t*)p;
+    const size_t need = (size_t)(dev::kQueueCounters + 1u) * stride;
+    std::lock_guard<std::mutex> lock(g_queue_mu);
+    if (!q.buf || q.slot_bytes < need) {
+        if (q.buf) {
+            (void)hipFree(q.buf);
+            q.buf = nullptr;
+        }
+        void* p = nullptr;
+        int rc = hip_check(hipMalloc(&p, (size_t)kQueueSlots * need), "rt_render: work queue allocation");
+        if (rc != RT_OK) return rc;
+        q.buf = (uint32_t*)p;
+        q.slot_bytes = need;
+        if (q.cus == 0) {
             int n = 0;
             rc = hip_check(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device),
                            "rt_render: compute unit count");
@@ -2633,7 +2630,7 @@ int acquire_queue(int device, uint32_t** head, int* cus) {
             q.cus = n;
         }
     }
-    *head = q.buf + (size_t)(q.next.fetch_add(1u) % kQueueSlots) * (kQueueBytes / 4u);
+    *head = q.buf + (size_t)(q.next.fetch_add(1u) % kQueueSlots) * (q.slot_bytes / 4u);
     *cus = q.cus;
     return RT_OK;
 }
@@ -2646,8 +2643,9 @@ using namespace rt;
 
 extern "C" {
 
-int rt_set_wave_trace(void* buffer) {
+int rt_set_wave_trace(void* buffer, uint64_t words) {
     g_wave_trace = (unsigned long long*)buffer;
+    g_wave_trace_words = buffer ? words : 0;
     return RT_OK;
 }
 
@@ -2783,15 +2781,6 @@ int rt_set_tuning(int key, int value) {
         g_flat_max = value;
         return prev;
     }
-    if (key == RT_TUNE_FLAT_RIUS_TRIPS) {
-        if (value < 0 || value > 64) {
-            set_error("rt_set_tuning: RandomInUnitSphere trips must be in [0, 64]");
-            return RT_ERR_INVALID_ARGUMENT;
-        }
-        int prev = g_flat_rius_trips;
-        g_flat_rius_trips = value;
-        return prev;
-    }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
         if (value < 0 || value > 16) {
             set_error("rt_set_tuning: persistent waves per SIMD must be in [0, 16]");
@@ -2878,6 +2867,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.rng_key_hi = (uint32_t)(a->rng_seed >> 32);
     P.rng_frame = a->rng_frame;
     P.wave_trace = g_wave_trace;
+    P.wave_trace_words = g_wave_trace_words;
     P.tile_order = g_tile_order;
     // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
     const rt_input_struct& in = a->inputs;
@@ -3020,8 +3010,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.prims = (const float4*)S.prims_flat;
         P.ref_nodes = (const float4*)S.ref_nodes;
     }
-    const int trips = V.kernel >= 5 ? g_flat_rius_trips : g_rius_trips;
-    P.rius_cap = trips > 0 ? (uint32_t)trips : 0xffffffffu;
+    P.rius_cap = g_rius_trips > 0 ? (uint32_t)g_rius_trips : 0xffffffffu;  // (the flat kernels')
     const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave
     P.tiles_x = (a->width + tile - 1) / tile;
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);
@@ -3030,7 +3019,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (persistent) {
         int device = 0, cus = 0, per_cu = 0;
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
-        if (rc == RT_OK) rc = acquire_queue(device, &P.work_counter, &cus);
+        if (rc == RT_OK) rc = acquire_queue(device, (uint32_t)g_queue_stride, &P.work_counter, &cus);
         if (rc == RT_OK)
             rc = hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, V.block, lds_bytes),
                            "rt_render: occupancy query");

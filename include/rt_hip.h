@@ -227,7 +227,10 @@ enum rt_render_flags {
     RT_FLAG_NO_STATE_WRITEBACK = 1u << 1, /* do not store the advanced RNG state (benchmark repeatability) */
     RT_FLAG_ACCUMULATE = 1u << 2, /* accum[px].rgb += Σ samples, accum[px].w += spp; pos shows rgb / w */
     RT_FLAG_RIUS_LEFT_TO_RIGHT = 1u << 3, /* fill Random()'s Vec3(ξ,ξ,ξ) left to right (default: right to
-                                             left, the order the survey's g++ build of Math.cuh:233 used) */
+                                             left, the order the survey's g++ build of Math.cuh:233 used — the
+                                             only build of the reference available here; C++ leaves the order
+                                             unspecified and nvcc's is not established).
+                                             Both orders are tested against the oracle on every config. */
     RT_FLAG_COUNT_TESTS = 1u << 4, /* also count box and primitive tests into counters[1], [2] */
     RT_FLAG_RNG_PHILOX = 1u << 5,  /* perf-mode RNG: each pixel draws from the hipRAND/rocRAND Philox4x32-10
                                       stream rocrand_init(rng_seed, subsequence = global pixel index,
@@ -281,10 +284,11 @@ float rt_last_kernel_ms(void);
  * any device update); < 0 before the first call. */
 float rt_last_launch_host_ms(void);
 
-/* Diagnostic (per thread): device buffer that later launches fill with s_memrealtime stamps (100 MHz): v3,
- * 2 × uint64 per 8×8 tile (its wave's start and end; tools/wave_timeline.py); v4, 4 × uint64 per persistent
- * wave (start, the moment its work queue ran dry, end, pixels taken; tools/v4_timeline.py).  NULL = off. */
-int rt_set_wave_trace(void* buffer);
+/* Diagnostic (per thread): device buffer of `words` uint64 that later launches fill with s_memrealtime stamps
+ * (100 MHz): v3 and flat, 2 per 8×8 tile (its wave's start and end; tools/wave_timeline.py); v4 and persistent flat,
+ * 4 per persistent wave (start, the moment its work queue ran dry, end, pixels taken; tools/v4_timeline.py).  Stamps
+ * that would fall beyond `words` are not written.  NULL = off. */
+int rt_set_wave_trace(void* buffer, uint64_t words);
 
 /* Experiment (per thread): device uint32 permutation of the frame's 8×8 tiles giving the v3 kernels' launch
  * order (NULL = row-major).  Results do not depend on it (every pixel is independent); the time does. */
@@ -323,19 +327,17 @@ int rt_last_variant(void);
  *   pixels still rendering (0 = off; 0..64; default 48).  The image does not depend on it.
  *   RT_TUNE_LEAF_BREAK: the v3 kernels leave the node-visit loop for the leaf tests once at most this many of
  *   the still-traversing lanes hold no leaf (0..64, default 3; 0 = once every lane holds one).  Nor does this.
- *   RT_TUNE_RIUS_TRIPS: the v3 kernels make at most this many RandomInUnitSphere attempts (Math.cuh:252-260) per
- *   shading pass; a lane whose attempts were all rejected continues the same call at the wave's next pass
- *   (0 = unbounded; 0..64; Philox mode rounds it up to whole blocks of four attempts).  The draws, and so the
- *   image, do not depend on it.
- *   RT_TUNE_FLAT_MAX: scenes of at most this many active primitives (0..64, default 16) run the flat kernel
- *   (variant 5: no BVH, every ray tests every primitive in the reference BVH's test order) where the automatic
- *   choice would run variant 3.  RT_TUNE_FLAT_RIUS_TRIPS: RT_TUNE_RIUS_TRIPS for the flat kernel (default 2).
- *   Neither changes the image. */
+ *   RT_TUNE_FLAT_MAX: scenes of at most this many active primitives (0..64, default 16) run the flat kernels
+ *   (variants 5 and 6: no BVH, every ray tests every primitive in the reference BVH's test order) where the
+ *   automatic choice would run variant 3 or 4.  RT_TUNE_RIUS_TRIPS: the flat kernels make at most this many
+ *   RandomInUnitSphere attempts (Math.cuh:252-260) per shading pass; a lane whose attempts were all rejected
+ *   continues the same call at the wave's next pass (0 = unbounded; 0..64; default 4; Philox mode rounds it up
+ *   to whole blocks of four attempts).  Neither changes the image. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
                      RT_TUNE_REGEN_LIVE_FRAC = 9, RT_TUNE_LEAF_BREAK = 10, RT_TUNE_RIUS_TRIPS = 11,
-                     RT_TUNE_FLAT_MAX = 12, RT_TUNE_FLAT_RIUS_TRIPS = 13 };
+                     RT_TUNE_FLAT_MAX = 12 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

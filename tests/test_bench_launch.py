@@ -30,6 +30,17 @@ def test_self_launch_spawns_n_ranks(gpus, config):
     assert lines[0]["world_size"] == gpus and lines[0]["frame_ok"] is True
 
 
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_default_line_carries_config4_block(gpus):
+    """the driver's default `bench.py --gpus N` (config 2) also measures BASELINE config 4 (the
+    7680x4320 frame split over the N ranks + the gather): the rehearsed launch carries other_configs.c4."""
+    p = _bench("--gpus", str(gpus), "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")][0]
+    c4 = line["other_configs"]["c4"]
+    assert c4["frame_ok"] is True and c4["height"] == 4320 and c4["scaling"] == "strong"
+
+
 def test_fewer_gpus_than_requested_fails_loudly():
     """The driver's `python bench.py --gpus N` must never print a 1-GPU line for N > 1 (this container has no GPU)."""
     p = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", timeout=120)

@@ -21,6 +21,10 @@ from oracle import py_oracle as po
 pytestmark = pytest.mark.gpu
 
 THREADS = 16  # the GPU box's CPU share
+# Random()'s Vec3(ξ, ξ, ξ) fill order (Math.cuh:231-234; unspecified in C++): right to left as the survey's g++ build of
+# the reference evaluated it (the library default), and left to right (RT_FLAG_RIUS_LEFT_TO_RIGHT).  Which one nvcc's
+# device front end produces is not established here, so every configured frame is checked in both.
+ORDERS = {"rtl": (0, 1), "ltr": (abi.RT_FLAG_RIUS_LEFT_TO_RIGHT, 0)}  # name: (render flag, oracle rius_order)
 
 
 def _global_rows(local_rows, band_rows, num_ranks, rank):
@@ -29,30 +33,40 @@ def _global_rows(local_rows, band_rows, num_ranks, rank):
 
 @pytest.fixture(scope="module")
 def c4_oracle_states():
+    """Per Random() fill order, the oracle's states of the C4 frame (33 M × 48 B, seeded with the global pixel index);
+    the tests of one order advance disjoint rows of it."""
     cfg = scenes.CONFIGS["c4"]
-    return po.init_states(cfg.width, cfg.height)  # 33 M × 48 B, seeded with the global pixel index
+    states = {}
+
+    def get(order):
+        if order not in states:
+            states[order] = po.init_states(cfg.width, cfg.height)
+        return states[order]
+    return get
 
 
+@pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("rank", [0, 3, 7])
-def test_c4_rank_share_rows_match_oracle(rank, c4_oracle_states):
+def test_c4_rank_share_rows_match_oracle(rank, order, c4_oracle_states):
+    flag, rius = ORDERS[order]
     cfg = scenes.CONFIGS["c4"]
     assert (cfg.width, cfg.height, cfg.spp, cfg.depth) == (7680, 4320, 128, 8)
     sc = scenes.builtin(cfg.scene)
     r = Renderer(cfg.width, cfg.height, band_rows=16, num_ranks=8, rank=rank)
     assert r.local_rows == (544 if rank < 6 else 528)  # 270 bands over 8 ranks: 34 or 33 bands each
     r.render_init()
-    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs())
+    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), flags=flag)
     torch.cuda.synchronize()
     img = r.image()
     # local rows 16k + 7 for k = 0, 11, 22, 32: global rows (8k + rank)·16 + 7 → one oracle call per spacing
     local = [16 * k + 7 for k in (0, 11, 22)]
     glob = _global_rows(local, 16, 8, rank)
-    st = c4_oracle_states  # each rank's rows are disjoint: sharing the array across ranks is safe
+    st = c4_oracle_states(order)  # each rank's rows are disjoint: the ranks of one order share the array
     ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
-                          rows=(glob[0], cfg.height), row_step=glob[1] - glob[0], threads=THREADS)
+                          rows=(glob[0], cfg.height), row_step=glob[1] - glob[0], threads=THREADS, rius_order=rius)
     last_l, last_g = 16 * 32 + 7, _global_rows([16 * 32 + 7], 16, 8, rank)[0]  # the last band of every rank
     ref_last, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
-                               rows=(last_g, last_g + 1), threads=THREADS)
+                               rows=(last_g, last_g + 1), threads=THREADS, rius_order=rius)
     ref[last_g] = ref_last[last_g]
     local, glob = local + [last_l], glob + [last_g]
     np.testing.assert_array_equal(img[local], ref[glob])
@@ -94,8 +108,10 @@ def c5_scene():
     return sc
 
 
+@pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("rng", ["xorwow", "philox"])
-def test_c5_progressive_moving_camera_bit_exact(rng, c5_scene):
+def test_c5_progressive_moving_camera_bit_exact(rng, order, c5_scene):
+    flag, rius = ORDERS[order]
     cfg = scenes.CONFIGS["c5"].scaled(192, 108)
     assert (cfg.spp, cfg.depth) == (1, 4)
     ds = DeviceScene(c5_scene)
@@ -108,17 +124,20 @@ def test_c5_progressive_moving_camera_bit_exact(rng, c5_scene):
         if reset:
             r.reset_accumulation()
             acc[:] = 0.0
-        r.render(ds, cfg.spp, cfg.depth, inp, flags=abi.RT_FLAG_ACCUMULATE, frame=frame if rng == "philox" else None)
+        r.render(ds, cfg.spp, cfg.depth, inp, flags=abi.RT_FLAG_ACCUMULATE | flag,
+                 frame=frame if rng == "philox" else None)
         torch.cuda.synchronize()
         ref, _, cnt = po.render(osc, cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st, accum=acc,
-                                philox=rng == "philox", frame=frame)
+                                philox=rng == "philox", frame=frame, rius_order=rius)
         np.testing.assert_array_equal(r.image(), ref, err_msg=f"frame {frame}")
         np.testing.assert_array_equal(r.accum.cpu().numpy(), acc, err_msg=f"frame {frame}")
     if st is not None:
         np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
 
 
-def test_c5_full_size_progressive_rows_match_oracle(c5_scene):
+@pytest.mark.parametrize("order", list(ORDERS))
+def test_c5_full_size_progressive_rows_match_oracle(order, c5_scene):
+    flag, rius = ORDERS[order]
     cfg = scenes.CONFIGS["c5"]
     ds = DeviceScene(c5_scene)
     r = Renderer(cfg.width, cfg.height)
@@ -132,11 +151,12 @@ def test_c5_full_size_progressive_rows_match_oracle(c5_scene):
         if reset:
             r.reset_accumulation()
             acc[:] = 0.0
-        r.render(ds, cfg.spp, cfg.depth, inp, flags=abi.RT_FLAG_ACCUMULATE)
+        r.render(ds, cfg.spp, cfg.depth, inp, flags=abi.RT_FLAG_ACCUMULATE | flag)
         torch.cuda.synchronize()
         # the oracle renders only the sampled rows; accumulation of the other rows is not compared
         ref, _, _ = po.render(osc, cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st, accum=acc,
-                              rows=(rows[0], cfg.height), row_step=rows[1] - rows[0], threads=THREADS)
+                              rows=(rows[0], cfg.height), row_step=rows[1] - rows[0], threads=THREADS,
+                              rius_order=rius)
         img = r.image()
         np.testing.assert_array_equal(img[rows], ref[rows], err_msg=f"frame {frame}")
         got_acc = r.accum.cpu().numpy().reshape(cfg.height, cfg.width, 4)
@@ -145,19 +165,21 @@ def test_c5_full_size_progressive_rows_match_oracle(c5_scene):
     assert hit_textured > 0
 
 
-def test_c3_configured_256spp_rows_match_oracle():
+@pytest.mark.parametrize("order", list(ORDERS))
+def test_c3_configured_256spp_rows_match_oracle(order):
+    flag, rius = ORDERS[order]
     cfg = scenes.CONFIGS["c3"]
     assert (cfg.width, cfg.height, cfg.spp, cfg.depth) == (3840, 2160, 256, 16)
     sc = scenes.builtin(cfg.scene)
     r = Renderer(cfg.width, cfg.height)
     r.render_init()
-    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs())
+    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), flags=flag)
     torch.cuda.synchronize()
     st = po.init_states(cfg.width, cfg.height)
     step = cfg.height // 12
     rows = list(range(5, cfg.height, step))
     ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
-                          rows=(5, cfg.height), row_step=step, threads=THREADS)
+                          rows=(5, cfg.height), row_step=step, threads=THREADS, rius_order=rius)
     np.testing.assert_array_equal(r.image()[rows], ref[rows])
     np.testing.assert_array_equal(r.states().reshape(cfg.height, cfg.width, -1)[rows, :, :6],
                                   st.reshape(cfg.height, cfg.width, -1)[rows, :, :6])

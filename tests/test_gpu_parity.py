@@ -283,8 +283,12 @@ def test_invalid_arguments_fail_loudly():
 # ---------------------------------------------------------------------------------------------------
 # Full-size configurations: size-independent properties
 # ---------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("ltr", [False, True], ids=["rtl", "ltr"])
 @pytest.mark.parametrize("config", ["c2", "c3"])
-def test_full_size_rows_match_oracle_and_tiles_are_invariant(config):
+def test_full_size_rows_match_oracle_and_tiles_are_invariant(config, ltr):
+    """Configs 2 and 3 at full size in both Random() fill orders (Math.cuh:231-234: right to left, the library
+    default, and left to right, RT_FLAG_RIUS_LEFT_TO_RIGHT)."""
+    flag = abi.RT_FLAG_RIUS_LEFT_TO_RIGHT if ltr else 0
     cfg = scenes.CONFIGS[config]
     if config == "c3":
         cfg = cfg.scaled(cfg.width, cfg.height, 16)  # 256 spp × 8.3 Mpx is minutes of CPU oracle; rows still full-width
@@ -292,7 +296,7 @@ def test_full_size_rows_match_oracle_and_tiles_are_invariant(config):
     ds = DeviceScene(sc)
     r = Renderer(cfg.width, cfg.height)
     r.render_init()
-    r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=flag)
     torch.cuda.synchronize()
     img = r.image()
     assert np.all((img >> 24) == 0xFF)
@@ -300,7 +304,7 @@ def test_full_size_rows_match_oracle_and_tiles_are_invariant(config):
     step = cfg.height // 6
     st = po.init_states(cfg.width, cfg.height)
     ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
-                          rows=(1, cfg.height), row_step=step, threads=16)
+                          rows=(1, cfg.height), row_step=step, threads=16, rius_order=0 if ltr else 1)
     rows = list(range(1, cfg.height, step))
     np.testing.assert_array_equal(img[rows], ref[rows])
     np.testing.assert_array_equal(r.states().reshape(cfg.height, cfg.width, -1)[rows, :, :6],
@@ -310,7 +314,7 @@ def test_full_size_rows_match_oracle_and_tiles_are_invariant(config):
     for rank in range(4):
         rr = Renderer(cfg.width, cfg.height, band_rows=16, num_ranks=4, rank=rank)
         rr.render_init()
-        rr.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+        rr.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=flag)
         torch.cuda.synchronize()
         full[rr.rows] = rr.image()
         del rr
@@ -399,8 +403,7 @@ def test_scene_beyond_16bit_references_matches_oracle(variant):
         r.render_init()
         r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
         torch.cuda.synchronize()
-        assert lib().rt_last_variant() == (variant if variant >= 0 else lib().rt_last_variant())
-        assert lib().rt_last_variant() in ((3, 4) if variant < 0 else (variant,))
+        assert lib().rt_last_variant() == variant if variant >= 0 else lib().rt_last_variant() in (3, 4)
     finally:
         lib().rt_set_variant(-1)
     ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(),
@@ -749,18 +752,17 @@ def test_persistent_queue_knobs_change_schedule_not_pixels(chunk, stride):
     assert int(r.counters[0]) == int(g["counters"][0])
 
 
-# v3 scheduling knobs (rt_hip.h): (key, value) pairs around the defaults, including the extremes
-V3_KNOBS = [(abi.RT_TUNE_RIUS_TRIPS, k) for k in (0, 1, 2, 3, 5)] + \
-           [(abi.RT_TUNE_LEAF_BREAK, k) for k in (0, 1, 64)] + \
-           [(abi.RT_TUNE_REGEN_LIVE_FRAC, k) for k in (0, 1, 64)]
+# scheduling knobs (rt_hip.h) and the kernels they steer: (key, value) pairs around the defaults, with the extremes
+V3_KNOBS = [(abi.RT_TUNE_LEAF_BREAK, k, v) for k in (0, 1, 64) for v in (2, 3)] + \
+           [(abi.RT_TUNE_REGEN_LIVE_FRAC, k, v) for k in (0, 1, 64) for v in (2, 3)] + \
+           [(abi.RT_TUNE_RIUS_TRIPS, k, v) for k in (0, 1, 2, 3, 5) for v in (5, 6)]
 
 
-@pytest.mark.parametrize("variant", [2, 3])
-@pytest.mark.parametrize("key, value", V3_KNOBS, ids=lambda v: str(v))
+@pytest.mark.parametrize("key, value, variant", V3_KNOBS, ids=lambda v: str(v))
 def test_v3_scheduling_knobs_change_schedule_not_pixels(key, value, variant):
-    """RT_TUNE_RIUS_TRIPS (a RandomInUnitSphere call split over shading passes), RT_TUNE_LEAF_BREAK and
-    RT_TUNE_REGEN_LIVE_FRAC decide when a v3 wave traverses, tests leaves or shades, never what a lane computes:
-    every setting renders the golden images, ray counts and advanced RNG states (XORWOW) and the Philox goldens."""
+    """RT_TUNE_LEAF_BREAK and RT_TUNE_REGEN_LIVE_FRAC decide when a v3 wave traverses, tests leaves or shades, and
+    RT_TUNE_RIUS_TRIPS when a flat-kernel lane resumes a RandomInUnitSphere call — never what a lane computes: every
+    setting renders the golden images, ray counts and advanced RNG states (XORWOW) and the Philox goldens."""
     prev = lib().rt_set_tuning(key, value)
     assert prev >= 0
     lib().rt_set_variant(variant)
@@ -770,9 +772,12 @@ def test_v3_scheduling_knobs_change_schedule_not_pixels(key, value, variant):
             cfg, g = case.cfg(), load_golden(case.name)
             r = Renderer(cfg.width, cfg.height)
             r.render_init()
-            r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
+            ds = DeviceScene(scenes.builtin(cfg.scene))
+            r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
             torch.cuda.synchronize()
-            assert lib().rt_last_variant() == variant
+            # (a scene beyond the flat kernels' 64 primitives, RTIOW's 488 spheres, runs v3 / v4 instead)
+            big = ds.info().num_primitives > 64
+            assert lib().rt_last_variant() == (variant - 2 if variant >= 5 and big else variant)
             np.testing.assert_array_equal(r.image(), g["pos"], err_msg=name)
             assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes(), name
             assert int(r.counters[0]) == int(g["counters"][0]), name

@@ -7,6 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
 bash tools/ab_variants_build.sh \
   'noexact=cudaraytracer_amd/csrc/render.hip:s/if (tie || nan || edge || t_best != t_best) {/if (false) {/' \
+  'inline=cudaraytracer_amd/csrc/render.hip:s/__device__ __noinline__ HitOut ref_trace/__device__ __forceinline__ HitOut ref_trace/' \
   > gpurun_out/abbuild.log 2>&1 || { tail -5 gpurun_out/abbuild.log; exit 3; }
 one() {  # lib label args
   RT_HIP_LIB=$1 timeout -k 10 200 python bench.py --no-cpu-baseline --no-philox-line --no-config-lines $3 > gpurun_out/ab.log 2>&1 || { tail -3 gpurun_out/ab.log; exit 4; }
@@ -14,9 +15,11 @@ one() {  # lib label args
 }
 LIB=cudaraytracer_amd/librt_hip.so
 for r in 1 2; do
-  one $LIB "c3 exact flat K=4" "--config c3 --steps 2 --warmup 1 --variant 5 --tune 13=4"
-  one /tmp/ablib/noexact.so "c3 noexact flat K=4" "--config c3 --steps 2 --warmup 1 --variant 5 --tune 13=4"
+  one $LIB "c3 exact flat K=4" "--config c3 --steps 2 --warmup 1 --variant 5 --tune 11=4"
+  one /tmp/ablib/noexact.so "c3 noexact flat K=4" "--config c3 --steps 2 --warmup 1 --variant 5 --tune 11=4"
+  one /tmp/ablib/inline.so "c3 inline flat K=4" "--config c3 --steps 2 --warmup 1 --variant 5 --tune 11=4"
   one $LIB "c5 exact persistent flat" "--config c5 --steps 20 --warmup 4 --variant 6"
   one /tmp/ablib/noexact.so "c5 noexact persistent flat" "--config c5 --steps 20 --warmup 4 --variant 6"
+  one /tmp/ablib/inline.so "c5 inline persistent flat" "--config c5 --steps 20 --warmup 4 --variant 6"
   one $LIB "c5 v4" "--config c5 --steps 20 --warmup 4 --variant 4"
 done

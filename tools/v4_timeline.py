@@ -45,10 +45,10 @@ def run(ds, cfg, spp, depth, flags, rng="xorwow", layout="soa", n=None, traced=T
         if r.accum is not None:
             r.reset_accumulation()
         trace.zero_()
-        lib().rt_set_wave_trace(trace.data_ptr() if traced else None)
+        lib().rt_set_wave_trace(trace.data_ptr() if traced else None, trace.numel())
         r.render(ds, spp, depth, inp, flags=flags)
         torch.cuda.synchronize()
-        lib().rt_set_wave_trace(None)
+        lib().rt_set_wave_trace(None, 0)
         times.append(lib().rt_last_kernel_ms())
         t = trace.cpu().numpy().reshape(-1, 4)
         t = t[t[:, 0] > 0].astype(np.float64)

@@ -23,10 +23,10 @@ buf = torch.zeros(2 * waves + 64, dtype=torch.int64, device="cuda")
 if args.warm:  # one untraced frame first: the traced frame then runs in the adaptive (longest-first) order
     r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
     torch.cuda.synchronize()
-lib().rt_set_wave_trace(buf.data_ptr())
+lib().rt_set_wave_trace(buf.data_ptr(), buf.numel())
 r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
 torch.cuda.synchronize()
-lib().rt_set_wave_trace(None)
+lib().rt_set_wave_trace(None, 0)
 t = buf[: 2 * waves].cpu().numpy().reshape(-1, 2).astype(np.float64)
 t = t[t[:, 0] > 0]
 t0 = t[:, 0].min()
