@@ -676,11 +676,12 @@ __device__ __forceinline__ void store_rng(const KParams& P, uint32_t* st, const 
 }
 
 template <class R>
-__device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32_t* st, const R& rng, f3 col) {
+__device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32_t* st, const R& rng, f3 col,
+                                            const float4* acc_pre = nullptr) {
     store_rng(P, st, rng);
     f3 c;
     if (P.flags & RT_FLAG_ACCUMULATE) {
-        float4 a = P.accum[pix];
+        float4 a = acc_pre ? *acc_pre : P.accum[pix];  // (acc_pre: the value loaded when the pixel started)
         a.x = a.x + col.x;
         a.y = a.y + col.y;
         a.z = a.z + col.z;
@@ -2040,7 +2041,9 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
     hit = -1;
     tag = 0u;
     t_best = FLT_MAX;
-    bool tie = false, nan = false;  // a candidate equal to the closest hit so far / an accepted NaN distance
+    // lanes where a candidate equals the closest hit so far / an accepted distance was NaN, as wave-uniform lane masks
+    // (scalar mask arithmetic, no per-lane VALU bookkeeping)
+    uint64_t tie_m = 0u, nan_m = 0u;
     const float a_dd = dot(rd, rd);
     const bool fast_div = a_dd >= 0x1p-40f && a_dd <= 0x1p40f;  // RN(1/a) for the sphere roots (div_rn)
     const float inv_a = rcp_rn(a_dd);
@@ -2056,8 +2059,9 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
         const float yy = ob + t * db;
         // (non-short-circuit & and |: lane-mask arithmetic, no branch)
         const bool acc = (!(t < kTmin) & !(t > t_best)) & (!(xx < q0.y) & !(xx > q0.z) & !(yy < q0.w) & !(yy > q1.x));
-        tie = (tie & !acc) | (acc & (t == t_best));
-        nan = nan | (acc & (t != t));
+        const uint64_t acc_m = __ballot(acc);
+        tie_m = (tie_m & ~acc_m) | (acc_m & __ballot(t == t_best));
+        nan_m |= acc_m & __ballot(t != t);
         t_best = acc ? t : t_best;
         hit = acc ? (int)i : hit;
         tag = acc ? __float_as_uint(q1.w) : tag;
@@ -2080,7 +2084,7 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
             const bool near_ok = (tn < t_best) & (tn > kTmin);
             const float t = near_ok ? tn : tf;  // the far root is tried only when the near one is out of range
             const bool acc = real & (t < t_best) & (t > kTmin);
-            tie = (tie | (real & ((tn == t_best) | (!near_ok & (tf == t_best))))) & !acc;
+            tie_m = (tie_m | __ballot(real & ((tn == t_best) | (!near_ok & (tf == t_best))))) & ~__ballot(acc);
             t_best = acc ? t : t_best;
             hit = acc ? (int)i : hit;
             tag = acc ? __float_as_uint(q1.w) : tag;
@@ -2122,6 +2126,7 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
             edge |= fabsf(ps[a] - lo) <= slack || fabsf(ps[a] - hi) <= slack;
         }
     }
+    const bool tie = (tie_m >> __lane_id()) & 1u, nan = (nan_m >> __lane_id()) & 1u;
     if (tie || nan || edge || t_best != t_best) {
         const HitOut r = ref_trace(rnodes, prims, ro, rd);
         hit = r.hit;
@@ -2209,13 +2214,25 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
 // grid whose lanes take the next pixel from the frame's work queue as soon as theirs is done (PixelQueue), for frames
 // with few samples per pixel (BASELINE config 5: 1 spp), where a tile wave would idle on its slowest pixels.  The path
 // state stays in registers (no traversal, nothing to park).  Requires spp >= 1 and max_depth >= 1 (rt_render).
+// Such a frame is bound by each pixel's chain of dependent memory round trips (RNG state, texel gathers, the
+// accumulator), so PREFETCH hides two of them: bit 0 — a lane that starts a pixel also takes its NEXT pixel from the
+// queue and issues that pixel's XORWOW state loads, consumed only when it starts it; bit 1 — the float4 accumulator
+// of the current pixel is loaded when it starts, not when it is written.
+constexpr int kFlatPrefetch = 1;
 template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persistent(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
+    constexpr bool kNext = (kFlatPrefetch & 1) && !PHILOX;  // (Philox has no per-pixel state to load)
+    constexpr bool kAcc = (kFlatPrefetch & 2) != 0;
+    constexpr uint32_t kNone = 0xffffffffu;
     const float4* __restrict__ prims = P.prims;  // the flat table (rt_render)
     const bool rtl = P.rius_rtl != 0;
+    const bool accumulate = (P.flags & RT_FLAG_ACCUMULATE) != 0;
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     R rng{};
+    Rng nrng{};               // kNext: the prefetched pixel's state (loads in flight until it starts)
+    uint32_t npix = kNone, nx = 0u, ng = 0u;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // kAcc: the current pixel's accumulator
     f3 col = mk(0.0f, 0.0f, 0.0f), att = col, ro = col, rd = col;
     uint32_t x = 0u, g = 0u, pix = 0u, sample = 0u, depth = 0u, rays = 0u;
     int mode = MODE_NEED;
@@ -2245,26 +2262,49 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
                 if (++sample < P.spp) {
                     cam = true;
                 } else {  // the pixel is done (Kernel.cu:149-157)
-                    write_pixel(P, pix, state_at(P, pix), rng, col);
+                    write_pixel(P, pix, state_at(P, pix), rng, col, kAcc && accumulate ? &acc : nullptr);
                     mode = MODE_NEED;
                 }
             } else if (res == SHADE_CONTINUE) {
                 mode = MODE_TRAV;
             }
         }
-        // pixel regeneration: lanes without a pixel take the next work indices
+        // pixel regeneration: a lane without a pixel starts its prefetched one, or takes the next work index
         bool need = mode == MODE_NEED;
         if (__ballot(need) != 0) {
-            queue.take(P, need, [&](uint32_t nx, uint32_t ng, uint32_t npix) {
-                x = nx;
-                g = ng;
-                pix = npix;
-                rng = begin_rng<R>(state_at(P, npix), P.state_stride, ng * P.width + nx);  // Kernel.cu:119-123
+            bool started = false;
+            const auto start = [&](uint32_t sx, uint32_t sg, uint32_t spix, const R& srng) {
+                x = sx;
+                g = sg;
+                pix = spix;
+                rng = srng;
+                if (kAcc && accumulate) acc = P.accum[spix];
                 col = mk(0.0f, 0.0f, 0.0f);
                 sample = 0u;
                 cam = true;
+                started = true;
+            };
+            if constexpr (kNext) {
+                if (need && npix != kNone) {
+                    need = false;
+                    start(nx, ng, npix, nrng);
+                    npix = kNone;
+                }
+            }
+            queue.take(P, need, [&](uint32_t qx, uint32_t qg, uint32_t qpix) {  // Kernel.cu:119-123
+                start(qx, qg, qpix, begin_rng<R>(state_at(P, qpix), P.state_stride, qg * P.width + qx));
             });
             if (need) mode = MODE_DONE;
+            if constexpr (kNext) {  // the next pixel of every lane that just started one: its state loads go out now
+                bool want = started && npix == kNone;
+                if (__ballot(want) != 0)
+                    queue.take(P, want, [&](uint32_t qx, uint32_t qg, uint32_t qpix) {
+                        nx = qx;
+                        ng = qg;
+                        npix = qpix;
+                        nrng = load_rng(state_at(P, qpix), P.state_stride);
+                    });
+            }
         }
         if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
             KParamsC* q = kparams_reload();

@@ -1,4 +1,4 @@
-"""Where a persistent-kernel (v4) frame's time goes: C5 (1 spp, depth 4/1) and C2 at 1 spp.
+"""Where a persistent-kernel (v4, or with --variant 6 the persistent flat kernel) frame's time goes: C5 (1 spp, depth 4/1) and C2 at 1 spp.
 
 For each case the frame is rendered with the v4 wave trace (rt_set_wave_trace: per persistent wave its start, the
 moment its work queue ran dry, its end and the pixels it took, s_memrealtime at 100 MHz) and timed with HIP events
@@ -24,6 +24,7 @@ from cudaraytracer_amd.renderer import DeviceScene, Renderer
 ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=12)
 ap.add_argument("--sweep", action="store_true")
+ap.add_argument("--variant", type=int, default=4, help="persistent kernel: 4 (v4, BVH) or 6 (persistent flat)")
 args = ap.parse_args()
 
 c5 = scenes.CONFIGS["c5"]
@@ -34,7 +35,7 @@ trace = torch.zeros(4 * 65536, dtype=torch.int64, device="cuda")
 
 def run(ds, cfg, spp, depth, flags, rng="xorwow", layout="soa", n=None, traced=True):
     n = n or args.frames
-    lib().rt_set_variant(4)
+    lib().rt_set_variant(args.variant)
     r = Renderer(cfg.width, cfg.height, rng=rng, state_layout=layout)
     r.render_init()
     times, spans = [], []
