@@ -2217,8 +2217,12 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
 // Such a frame is bound by each pixel's chain of dependent memory round trips (RNG state, texel gathers, the
 // accumulator), so PREFETCH hides two of them: bit 0 — a lane that starts a pixel also takes its NEXT pixel from the
 // queue and issues that pixel's XORWOW state loads, consumed only when it starts it; bit 1 — the float4 accumulator
-// of the current pixel is loaded when it starts, not when it is written.
+// of the current pixel is loaded when it starts, not when it is written.  The next pixel is taken early only while
+// the wave's queue head holds more than 1/kPrefetchStop of its range: near the end a pixel parked in a busy lane's
+// prefetch slot waits out that lane's current pixel while other lanes idle (always-on prefetch lengthened the tail
+// 168 -> 211 us; profiles/r04e_ab_c5_prefetch.txt).
 constexpr int kFlatPrefetch = 1;
+constexpr uint32_t kPrefetchStop = 8;
 template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persistent(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
@@ -2296,7 +2300,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
             });
             if (need) mode = MODE_DONE;
             if constexpr (kNext) {  // the next pixel of every lane that just started one: its state loads go out now
-                bool want = started && npix == kNone;
+                bool want = started && npix == kNone && queue.head_left > P.work_per_counter / kPrefetchStop;
                 if (__ballot(want) != 0)
                     queue.take(P, want, [&](uint32_t qx, uint32_t qg, uint32_t qpix) {
                         nx = qx;

@@ -15,6 +15,7 @@ import pytest
 import torch
 
 from cudaraytracer_amd import abi, scenes
+from cudaraytracer_amd._lib import lib
 from cudaraytracer_amd.renderer import DeviceScene, Renderer
 from oracle import py_oracle as po
 
@@ -386,3 +387,31 @@ def test_launch_kernel_cache_follows_the_texel_layout():
             np.testing.assert_array_equal(img, ref, err_msg=f"texel layout {layout}")
     finally:
         lib().rt_set_tuning(6, prev)
+
+
+@pytest.mark.parametrize("config, spp, variant", [("c2", 64, 3), ("c3", 16, 5), ("c3", 16, 6), ("c5", 1, 6), ("c1", 4, 5)])
+def test_whole_frame_bit_exact(config, spp, variant):
+    """Every pixel, every advanced RNG state and the ray count of a full-size frame against the oracle's whole frame
+    (not row samples): C2 as configured on v3, C3 at full resolution (16 of its 256 spp: the CPU oracle's share of the
+    test budget) on both flat kernels, whose reference replay makes the box-face and tie rays exact, C5 and C1.
+    (tools/full_frame_parity.py runs the same comparison at 256 spp: profiles/r04c_full_frame_parity.jsonl.)"""
+    cfg = scenes.CONFIGS[config]
+    cfg = cfg.scaled(cfg.width, cfg.height, spp)
+    sc = cfg.scene_desc() if config == "c5" else scenes.builtin(cfg.scene)
+    inp = scenes.camera_inputs(*scenes.moving_camera(0, 60), cfg.fov) if config == "c5" else cfg.inputs()
+    lib().rt_set_variant(variant)
+    try:
+        r = Renderer(cfg.width, cfg.height)
+        r.render_init()
+        r.render(DeviceScene(sc), cfg.spp, cfg.depth, inp)
+        torch.cuda.synchronize()
+        assert lib().rt_last_variant() == variant
+    finally:
+        lib().rt_set_variant(-1)
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st, threads=THREADS)
+    img = r.image()
+    bad = np.argwhere(img != ref)
+    assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
+    np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
+    assert int(r.counters[0]) == cnt.rays

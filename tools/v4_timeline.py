@@ -24,6 +24,8 @@ from cudaraytracer_amd.renderer import DeviceScene, Renderer
 ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=12)
 ap.add_argument("--sweep", action="store_true")
+ap.add_argument("--detail", action="store_true", help="per-wave percentiles of the dry and end times")
+ap.add_argument("--cases", type=int, default=0, help="only the first N cases (0: all)")
 ap.add_argument("--variant", type=int, default=4, help="persistent kernel: 4 (v4, BVH) or 6 (persistent flat)")
 args = ap.parse_args()
 
@@ -68,7 +70,8 @@ def run(ds, cfg, spp, depth, flags, rng="xorwow", layout="soa", n=None, traced=T
     d = dict(ms=ms, waves=len(t), span_us=span, launch_us=ms * 1e3 - span, ramp_us=start.max(),
              ramp90_us=np.percentile(start, 90), steady_us=dry.min() - start.max(), tail_us=span - dry.min(),
              px_median=np.median(px), px_p10=np.percentile(px, 10), px_p90=np.percentile(px, 90),
-             life_median_us=np.median(end - start))
+             life_median_us=np.median(end - start), dry_pct=np.percentile(dry, [10, 50, 90, 99]),
+             end_pct=np.percentile(end, [10, 50, 90, 99]))
     return ms, d
 
 
@@ -81,6 +84,10 @@ def show(name, res):
           f"(p90 {d['ramp90_us']:.1f}), steady {d['steady_us']:.1f}, tail {d['tail_us']:.1f} (span {d['span_us']:.1f}) | "
           f"pixels/wave p10/50/90 {d['px_p10']:.0f}/{d['px_median']:.0f}/{d['px_p90']:.0f}, wave life "
           f"{d['life_median_us']:.1f} us", flush=True)
+    if args.detail:
+        f = lambda a: "/".join(f"{v:.0f}" for v in a)
+        print(f"{'':52s} wave dry p10/50/90/99 {f(d['dry_pct'])} us, wave end p10/50/90/99 {f(d['end_pct'])} us",
+              flush=True)
 
 
 acc = abi.RT_FLAG_ACCUMULATE
@@ -90,7 +97,7 @@ cases = [("c5 1 spp depth 4 (as configured)", dict(ds=ds5, cfg=c5, spp=1, depth=
          ("c5 depth 4, philox (no state)", dict(ds=ds5, cfg=c5, spp=1, depth=4, flags=acc, rng="philox")),
          ("c5 depth 1, philox, no accumulation", dict(ds=ds5, cfg=c5, spp=1, depth=1, flags=0, rng="philox")),
          ("c2 scene 1 spp depth 8", dict(ds=ds2, cfg=scenes.CONFIGS["c2"], spp=1, depth=8, flags=0))]
-for name, kw in cases:
+for name, kw in cases[:args.cases or None]:
     show(name, run(**kw))
     show(name + " [untraced]", run(traced=False, **kw))
 
