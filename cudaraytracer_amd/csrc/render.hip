@@ -2481,6 +2481,7 @@ constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of t
 constexpr int kPhiloxCompactWaves = 8;  // ... of the non-texture Philox build of variant 3
 
 constexpr int kFlatWaves = 8;  // __launch_bounds__ waves per SIMD of the untextured flat kernel
+constexpr int kFlatPersistentWaves = 4;  // resident waves per SIMD of the persistent flat kernel's grid
 template <bool PH>
 KernelFn flat_pick(bool count, bool tex, bool persistent) {
     if (persistent) {
@@ -3072,6 +3073,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.work_chunk = (uint32_t)g_queue_chunk;
         P.queue_stride = (uint32_t)g_queue_stride / 4u;
         P.work_per_counter = (tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
+        // the persistent flat kernel runs 4 waves per SIMD even where its registers allow 5-6: C5 0.294 vs 0.307 ms
+        // (XORWOW), 0.300 vs 0.314 (Philox), 3 rounds on one box (profiles/r04f_ab_pflat_waves.txt)
+        if (V.kernel == 6) per_cu = std::min(per_cu, kFlatPersistentWaves * 4 * 64 / V.block);
         if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
         grid = (uint32_t)(resident < grid ? resident : grid);

@@ -309,8 +309,8 @@ int rt_last_variant(void);
  *   RT_TUNE_REGEN_THRESHOLD: resumable kernels leave traversal to shade/regenerate finished lanes when
  *   fewer than this many of a wave's 64 lanes are still tracing (1..64, default 56). */
 /*   RT_TUNE_LEAF_MAX: maximum primitives per BVH leaf used by later rt_scene_create calls (1..4, default 4). */
-/*   RT_TUNE_PERSISTENT_WAVES: waves per SIMD of the persistent kernels' grid (0 = occupancy query, default;
- *   1..16). */
+/*   RT_TUNE_PERSISTENT_WAVES: waves per SIMD of the persistent kernels' grid (0 = default: the occupancy query,
+ *   capped at 4 for the persistent flat kernel; 1..16). */
 /*   RT_TUNE_SAH_TRAVERSAL: cost of a node visit relative to a primitive test in the SAH leaf decision, ×10
   *   (1..1000, default 16), used by later rt_scene_create calls. */
 /*   RT_TUNE_LDS_PAD: diagnostic, extra LDS bytes per wave of the v3/v4 kernels (occupancy experiments; 0).

@@ -1,4 +1,6 @@
-"""Where a C5 frame's 0.54 ms goes: the configured frame against variants with one ingredient removed."""
+"""Where a C5 frame's time goes: the configured frame against variants with one ingredient removed (round 4 adds
+the texel-fetch cases: the same frame with 256x128 images, which stay cache-resident, and with constant albedos).
+  python tools/c5_diag.py [--quick]   (--quick: only the configured frame and the texture cases)"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -34,8 +36,19 @@ def frames(ds, cfg, flags, variant=-1, layout="curand", rng="xorwow", spp=None, 
 c5 = scenes.CONFIGS["c5"]
 ds5 = DeviceScene(c5.scene_desc())
 ds2 = DeviceScene(scenes.builtin(scenes.CONFIGS["c2"].scene))
+ds5_small = DeviceScene(scenes.builtin(c5.scene, texture_size=(256, 128)))
+flat = scenes.builtin(c5.scene, texture_size=(256, 128))
+for k in range(len(flat.materials)):
+    flat.materials[k].albedo.type, flat.materials[k].albedo.image = abi.RT_CONSTANT, -1
+ds5_const = DeviceScene(flat)
 acc = abi.RT_FLAG_ACCUMULATE
-for name, kw in [("c5 as configured (v4, accumulate, curand states)", dict(ds=ds5, flags=acc)),
+quick = "--quick" in sys.argv
+cases = [("c5 as configured (auto kernel, accumulate, curand states)", dict(ds=ds5, flags=acc)),
+         ("  256x128 textures (cache-resident texels)", dict(ds=ds5_small, flags=acc)),
+         ("  constant albedos (no texel fetch, no sphere uv)", dict(ds=ds5_const, flags=acc)),
+         ("  256x128 textures, philox, no accumulation", dict(ds=ds5_small, flags=0, rng="philox")),
+         ("  philox, no accumulation", dict(ds=ds5, flags=0, rng="philox"))]
+for name, kw in cases + ([] if quick else [("c5 as configured (v4, accumulate, curand states)", dict(ds=ds5, flags=acc, variant=4)),
                  ("  no accumulation", dict(ds=ds5, flags=0)),
                  ("  plane state layout", dict(ds=ds5, flags=acc, layout="soa")),
                  ("  philox (no state)", dict(ds=ds5, flags=acc, rng="philox")),
@@ -43,10 +56,12 @@ for name, kw in [("c5 as configured (v4, accumulate, curand states)", dict(ds=ds
                  ("  depth 1", dict(ds=ds5, flags=acc, depth=1)),
                  ("  4 spp", dict(ds=ds5, flags=acc, spp=4)),
                  ("  RTIOW scene (no textures) 1 spp depth 4", dict(ds=ds2, flags=acc)),
-                 ("  RTIOW scene, no accumulation, philox", dict(ds=ds2, flags=0, rng="philox"))]:
+                 ("  RTIOW scene, no accumulation, philox", dict(ds=ds2, flags=0, rng="philox"))]):
     ms, rays = frames(cfg=c5, **kw)
     print(f"{name:55s} {ms:7.3f} ms  {rays / 1e6:6.2f} M rays  {rays / ms / 1e6:6.2f} Gray/s", flush=True)
 
+if quick:
+    sys.exit(0)
 # host-side cost of one rt_render call (no synchronisation inside) and the kernel's own time (HIP events
 # recorded by librt_hip.so right around the launch, rt_set_timing)
 import time
