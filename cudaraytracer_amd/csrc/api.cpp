@@ -63,7 +63,8 @@ static void free_device(DeviceScene* s) {
     if (s->prims) (void)hipFree((void*)s->prims);
     if (s->prims_flat) (void)hipFree((void*)s->prims_flat);
     if (s->ref_nodes) (void)hipFree((void*)s->ref_nodes);
-    s->prims_flat = s->ref_nodes = nullptr;
+    if (s->flat_boxes) (void)hipFree((void*)s->flat_boxes);
+    s->prims_flat = s->ref_nodes = s->flat_boxes = nullptr;
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);  // texels: owned by rt_scene::texel_block
     s->nodes = s->prims = s->mats = nullptr;
@@ -91,6 +92,8 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.prims_flat = p;
     if ((rc = upload(h.ref_nodes, &p, "hipMalloc/hipMemcpy(ref_nodes)"))) goto fail;
     d.ref_nodes = p;
+    if ((rc = upload(h.flat_boxes, &p, "hipMalloc/hipMemcpy(flat_boxes)"))) goto fail;
+    d.flat_boxes = p;
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
     d.mats = p;
     if ((rc = upload(h.imgs, &p, "hipMalloc/hipMemcpy(images)"))) goto fail;
@@ -109,7 +112,7 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;
     d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs.size() + h.prims.size() + h.prims_flat.size() + h.ref_nodes.size() +
-                      h.mats.size()) * 4 +
+                      h.flat_boxes.size() + h.mats.size()) * 4 +
                      h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;

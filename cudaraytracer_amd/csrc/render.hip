@@ -248,6 +248,7 @@ struct KParams {
     uint32_t leaf_break;             // v3: leave the node loop once at most this many lanes still lack a leaf
     uint32_t rius_cap;               // flat: RandomInUnitSphere attempts per shading pass (0xffffffff = unbounded)
     const float4* ref_nodes;         // flat kernel: the reference BVH over the flat table (ref_trace)
+    const float4* flat_boxes;        // flat kernel: per flat record its reference box (flat_trace's exactness check)
 };
 
 constexpr int kStackMax = 64;
@@ -2032,23 +2033,30 @@ __device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, cons
 // boxes contain p*'s own (SurroundingBox), so only if p*'s hit point lies on or within rounding of a face of p*'s own
 // box: within 2^-18 relative of a face in the axes where t* and the box test compute differently, or a slab distance
 // of the rect's own plane axis equal to t* (both are (plane - o) · (1/d), monotone in the plane), — or (b) another
-// primitive ties with t* (which one the reference keeps depends on its culling and order), or (c) a NaN took part.
-// Those rays (about 1e-5 of them) replay the reference exactly (ref_trace); the rest are exact as they stand.
+// primitive ties with t* (which one the reference keeps depends on its culling and order), or (c) a NaN took part:
+// a rectangle's t is NaN only as 0 · inf, so only on rays with a zero or infinite direction component or a
+// non-finite origin (geometry is finite, scene_build.cpp), which are all replayed.  Those rays (about 1e-5 of them)
+// replay the reference exactly (ref_trace); the rest are exact as they stand.
 template <bool COUNT_TESTS>
 __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, const float4* __restrict__ rnodes,
-                                           const uint32_t n, const f3 ro, const f3 rd, int& hit, uint32_t& tag,
-                                           float& t_best, Counts& cnt) {
+                                           const float4* __restrict__ boxes, const uint32_t n, const f3 ro,
+                                           const f3 rd, int& hit, uint32_t& tag, float& t_best, Counts& cnt) {
     hit = -1;
     tag = 0u;
     t_best = FLT_MAX;
-    // lanes where a candidate equals the closest hit so far / an accepted distance was NaN, as wave-uniform lane masks
-    // (scalar mask arithmetic, no per-lane VALU bookkeeping)
-    uint64_t tie_m = 0u, nan_m = 0u;
+    // lanes where a candidate equals the closest hit so far, as a wave-uniform lane mask (scalar mask arithmetic, no
+    // per-lane VALU bookkeeping)
+    uint64_t tie_m = 0u;
     const float a_dd = dot(rd, rd);
     const bool fast_div = a_dd >= 0x1p-40f && a_dd <= 0x1p40f;  // RN(1/a) for the sphere roots (div_rn)
     const float inv_a = rcp_rn(a_dd);
     // 1.0f / d of each axis (the rect tests' inv_d*, Hittable.cuh:149), once per ray instead of once per rect
     const float ix = rcp_ieee(rd.x), iy = rcp_ieee(rd.y), iz = rcp_ieee(rd.z);
+    // (c): every 1/d component finite and non-zero and a finite origin, or the ray is replayed
+    // (x · 0 is NaN exactly when x is infinite or NaN)
+    const float z = __builtin_fmaf(ix, 0.0f, __builtin_fmaf(iy, 0.0f, __builtin_fmaf(iz, 0.0f, __builtin_fmaf(
+                        ro.x, 0.0f, __builtin_fmaf(ro.y, 0.0f, ro.z * 0.0f)))));
+    const bool odd = !(z == 0.0f) || ix == 0.0f || iy == 0.0f || iz == 0.0f;
     // Both tests branch-free: every lane evaluates the whole test and the closest hit moves by selects (the tests'
     // results are those of the reference's branches: x and y are pure functions of t, computed whatever t is).
     // XY/XZ/YZRect::Hit (Hittable.cuh:140-169, 196-225, 252-281) with the plane axis k and in-plane axes a, b
@@ -2061,7 +2069,6 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
         const bool acc = (!(t < kTmin) & !(t > t_best)) & (!(xx < q0.y) & !(xx > q0.z) & !(yy < q0.w) & !(yy > q1.x));
         const uint64_t acc_m = __ballot(acc);
         tie_m = (tie_m & ~acc_m) | (acc_m & __ballot(t == t_best));
-        nan_m |= acc_m & __ballot(t != t);
         t_best = acc ? t : t_best;
         hit = acc ? (int)i : hit;
         tag = acc ? __float_as_uint(q1.w) : tag;
@@ -2096,38 +2103,28 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
             rect(q0, q1, i, ro.x, ix, ro.y, rd.y, ro.z, rd.z);
         }
     }
-    // (a): p*'s hit point against the faces of p*'s own reference box
+    // (a): p*'s hit point against the faces of p*'s own reference box (boxes: scene_build.cpp pack_flat_box)
     bool edge = false;
     if (hit >= 0) {
-        const float4 q0 = prims[2 * hit], q1 = prims[2 * hit + 1];
+        const float4 lo = boxes[2 * hit], hi = boxes[2 * hit + 1];
+        // a rect's plane axis: its box's slab distances (k -/+ 0.0001 - o) · (1/d) against t* = (k - o) · (1/d)
+        // (lo.w, hi.w: NaN for a sphere)
         const uint32_t type = tag & 15u;
-        const float ps[3] = {ro.x + t_best * rd.x, ro.y + t_best * rd.y, ro.z + t_best * rd.z};
-        const float os[3] = {ro.x, ro.y, ro.z}, ds[3] = {rd.x, rd.y, rd.z}, is[3] = {ix, iy, iz};
-        const int k = type == RT_SPHERE ? -1 : (type == RT_XYRECT ? 2 : (type == RT_XZRECT ? 1 : 0));
-        const int ia = k == 0 ? 1 : 0;  // the rect's first in-plane axis (a0, a1; the other holds b0, b1)
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-            float lo, hi;
-            if (k < 0) {
-                lo = q0.x - q0.w;  // (component a below)
-                hi = q0.x + q0.w;
-                if (a == 1) lo = q0.y - q0.w, hi = q0.y + q0.w;
-                if (a == 2) lo = q0.z - q0.w, hi = q0.z + q0.w;
-            } else if (a == k) {
-                // the plane axis: the slab distances (k -/+ 0.0001 - o) · (1/d) bracket t* = (k - o) · (1/d)
-                const float e0 = ((q0.x - 0.0001f) - os[a]) * is[a], e1 = ((q0.x + 0.0001f) - os[a]) * is[a];
-                edge |= e0 == t_best || e1 == t_best;
-                continue;
-            } else {
-                lo = a == ia ? q0.y : q0.w;
-                hi = a == ia ? q0.z : q1.x;
-            }
-            const float slack = 0x1p-18f * (fabsf(os[a]) + fabsf(t_best * ds[a]) + fabsf(lo) + fabsf(hi)) + 0x1p-120f;
-            edge |= fabsf(ps[a] - lo) <= slack || fabsf(ps[a] - hi) <= slack;
-        }
+        const bool kz = type == RT_XYRECT, ky = type == RT_XZRECT;
+        const float ok = kz ? ro.z : (ky ? ro.y : ro.x), ik = kz ? iz : (ky ? iy : ix);
+        edge = ((lo.w - ok) * ik) == t_best || ((hi.w - ok) * ik) == t_best;
+        // the other faces, within 2^-18 relative (a rect's plane axis holds 1e30 there: never within)
+        const auto near_face = [&](const float o, const float d, const float l, const float h) {
+            const float td = t_best * d;
+            const float p = o + td;
+            const float slack = 0x1p-18f * (fabsf(o) + fabsf(td) + fabsf(l) + fabsf(h)) + 0x1p-120f;
+            return fabsf(p - l) <= slack || fabsf(p - h) <= slack;
+        };
+        edge = edge || near_face(ro.x, rd.x, lo.x, hi.x) || near_face(ro.y, rd.y, lo.y, hi.y) ||
+               near_face(ro.z, rd.z, lo.z, hi.z);
     }
-    const bool tie = (tie_m >> __lane_id()) & 1u, nan = (nan_m >> __lane_id()) & 1u;
-    if (tie || nan || edge || t_best != t_best) {
+    const bool tie = (tie_m >> __lane_id()) & 1u;
+    if (tie || odd || edge || t_best != t_best) {
         const HitOut r = ref_trace(rnodes, prims, ro, rd);
         hit = r.hit;
         tag = r.tag;
@@ -2182,7 +2179,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
     while (__ballot(mode != MODE_DONE) != 0) {
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
-            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.num_prims, ro, rd, hit, tag, t, cnt);
+            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.flat_boxes, P.num_prims, ro, rd, hit, tag, t, cnt);
             mode = MODE_SHADE;
         }
         if (mode == MODE_SHADE) {
@@ -2248,7 +2245,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     while (true) {
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
-            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.num_prims, ro, rd, hit, tag, t, cnt);
+            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.flat_boxes, P.num_prims, ro, rd, hit, tag, t, cnt);
             mode = MODE_SHADE;
         }
         bool cam = false;
@@ -3054,6 +3051,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (V.kernel == 5 || V.kernel == 6) {  // the flat kernels' tables: primitives in the reference's test order, its BVH
         P.prims = (const float4*)S.prims_flat;
         P.ref_nodes = (const float4*)S.ref_nodes;
+        P.flat_boxes = (const float4*)S.flat_boxes;
     }
     P.rius_cap = g_rius_trips > 0 ? (uint32_t)g_rius_trips : 0xffffffffu;  // (the flat kernels')
     const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave

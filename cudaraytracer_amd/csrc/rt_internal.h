@@ -72,6 +72,8 @@ struct HostScene {
     std::vector<float> prims_flat;     // scenes of <= kFlatMaxPrims primitives: the records in the reference BVH's
                                        // test order (the flat kernel's table), else empty
     std::vector<float> ref_nodes;      // ... and the reference BVH itself: 8 floats per node (scene_build.cpp)
+    std::vector<float> flat_boxes;     // ... and per flat record its reference box for the flat kernels' exactness
+                                       // check: 8 floats (scene_build.cpp)
 };
 
 // Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.  with_texels = false computes

@@ -16,6 +16,7 @@ struct DeviceScene {
     const void* prims = nullptr;   // float4 × 2 per primitive
     const void* prims_flat = nullptr;  // the same records in the reference BVH's test order (small scenes), or NULL
     const void* ref_nodes = nullptr;   // the reference BVH (boxes + shape) over prims_flat, or NULL
+    const void* flat_boxes = nullptr;  // per prims_flat record its reference box (exactness check), or NULL
     const void* mats = nullptr;    // float4 × 3 per material
     const void* imgs = nullptr;    // int4 per image
     const void* texels = nullptr;  // RGB8

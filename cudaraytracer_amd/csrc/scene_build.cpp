@@ -7,6 +7,7 @@
 // SAH build over padded reference boxes produces a BVH with the same closest-hit semantics: the
 // primitive tests alone decide the hit, boxes only cull (see rt_internal.h).
 #include <algorithm>
+#include <limits>
 #include <functional>
 #include <array>
 #include <cmath>
@@ -248,6 +249,23 @@ void ref_prim_box(const rt_hittable_desc& h, float lo[3], float hi[3]) {
     volatile float k = g.k;
     lo[g.ik] = k - 0.0001f;
     hi[g.ik] = k + 0.0001f;
+}
+
+// The flat kernels' exactness check (render.hip flat_trace) per flat record: (lo.xyz, kl), (hi.xyz, kh) — the record's
+// own reference box, except that a rectangle's plane axis holds 1e30 in lo/hi (its faces are checked through the
+// slab distances instead, kl / kh = k -/+ 0.0001f as AABB::Hit has them) and a sphere's kl / kh are NaN (no plane).
+void pack_flat_box(const rt_hittable_desc& h, float* o) {
+    float lo[3], hi[3];
+    ref_prim_box(h, lo, hi);
+    float kl = std::numeric_limits<float>::quiet_NaN(), kh = kl;
+    if (h.type != RT_SPHERE) {
+        const RectGeom g = rect_geom(h);
+        kl = lo[g.ik];
+        kh = hi[g.ik];
+        lo[g.ik] = hi[g.ik] = 1e30f;
+    }
+    o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2]; o[3] = kl;
+    o[4] = hi[0]; o[5] = hi[1]; o[6] = hi[2]; o[7] = kh;
 }
 int build_reference_tree(const rt_hittable_desc* h, std::vector<int>& objs, int b, int e, uint32_t depth,
                          std::vector<RefNode>* nodes) {
@@ -559,9 +577,11 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
             reference_test_order(rn, 0, &ord);
             std::vector<int> flat_index(desc->num_hittables, -1);
             out->prims_flat.resize(ord.size() * 8);
+            out->flat_boxes.resize(ord.size() * 8);
             for (size_t i = 0; i < ord.size(); i++) {
                 flat_index[ord[i]] = (int)i;
                 pack_prim(desc->hittables[ord[i]], out->prims_flat.data() + i * 8);
+                pack_flat_box(desc->hittables[ord[i]], out->flat_boxes.data() + i * 8);
             }
             // per node: (lo.xyz, child 0) (hi.xyz, child 1); a primitive child is ~(its flat index)
             out->ref_nodes.resize(rn.size() * 8);
