@@ -2034,9 +2034,9 @@ __device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, cons
 // box: within 2^-18 relative of a face in the axes where t* and the box test compute differently, or a slab distance
 // of the rect's own plane axis equal to t* (both are (plane - o) · (1/d), monotone in the plane), — or (b) another
 // primitive ties with t* (which one the reference keeps depends on its culling and order), or (c) a NaN took part:
-// a rectangle's t is NaN only as 0 · inf, so only on rays with a zero or infinite direction component or a
-// non-finite origin (geometry is finite, scene_build.cpp), which are all replayed.  Those rays (about 1e-5 of them)
-// replay the reference exactly (ref_trace); the rest are exact as they stand.
+// a rectangle's t is NaN only as 0 · inf, so only on rays with a zero or infinite 1/d component or a non-finite
+// origin (geometry is finite, scene_build.cpp); a wave holding such a ray re-runs the rectangles' t for it after the
+// scan.  Those rays (about 1e-5 of them) replay the reference exactly (ref_trace); the rest are exact as they stand.
 template <bool COUNT_TESTS>
 __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, const float4* __restrict__ rnodes,
                                            const float4* __restrict__ boxes, const uint32_t n, const f3 ro,
@@ -2052,7 +2052,7 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
     const float inv_a = rcp_rn(a_dd);
     // 1.0f / d of each axis (the rect tests' inv_d*, Hittable.cuh:149), once per ray instead of once per rect
     const float ix = rcp_ieee(rd.x), iy = rcp_ieee(rd.y), iz = rcp_ieee(rd.z);
-    // (c): every 1/d component finite and non-zero and a finite origin, or the ray is replayed
+    // (c): a rectangle's t can be NaN only if a 1/d component is infinite or zero or the origin is not finite
     // (x · 0 is NaN exactly when x is infinite or NaN)
     const float z = __builtin_fmaf(ix, 0.0f, __builtin_fmaf(iy, 0.0f, __builtin_fmaf(iz, 0.0f, __builtin_fmaf(
                         ro.x, 0.0f, __builtin_fmaf(ro.y, 0.0f, ro.z * 0.0f)))));
@@ -2123,8 +2123,21 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
         edge = edge || near_face(ro.x, rd.x, lo.x, hi.x) || near_face(ro.y, rd.y, lo.y, hi.y) ||
                near_face(ro.z, rd.z, lo.z, hi.z);
     }
+    // (c) for the rare waves holding such a ray: the rectangles' t once more (the scan's expression), NaN or not
+    bool nan = false;
+    if (__ballot(odd) != 0) {
+        for (uint32_t i = 0; i < n; i++) {
+            const ConstF32* q = (const ConstF32*)((const ConstU8*)prims + i * 32u);
+            const uint32_t type = __float_as_uint(q[7]) & 15u;
+            if (type == RT_SPHERE) continue;
+            const float ok = type == RT_XYRECT ? ro.z : (type == RT_XZRECT ? ro.y : ro.x);
+            const float ik = type == RT_XYRECT ? iz : (type == RT_XZRECT ? iy : ix);
+            const float t = (q[0] - ok) * ik;
+            nan = nan || (odd && t != t);
+        }
+    }
     const bool tie = (tie_m >> __lane_id()) & 1u;
-    if (tie || odd || edge || t_best != t_best) {
+    if (tie || nan || edge || t_best != t_best) {
         const HitOut r = ref_trace(rnodes, prims, ro, rd);
         hit = r.hit;
         tag = r.tag;

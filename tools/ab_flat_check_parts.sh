@@ -7,8 +7,8 @@ mkdir -p gpurun_out; export TMPDIR=/tmp
 SRC=cudaraytracer_amd/csrc/render.hip
 bash tools/ab_variants_build.sh \
   "noedge=$SRC:s/^    if (hit >= 0) {$/    if (false) {/" \
-  "notie=$SRC:s/if (tie || odd || edge || t_best != t_best) {/if (edge || t_best != t_best) {/" \
-  "noexact=$SRC:s/if (tie || odd || edge || t_best != t_best) {/if (false) {/" \
+  "notie=$SRC:s/if (tie || nan || edge || t_best != t_best) {/if (edge || t_best != t_best) {/" \
+  "noexact=$SRC:s/if (tie || nan || edge || t_best != t_best) {/if (false) {/" \
   > gpurun_out/abbuild.log 2>&1 || { tail -5 gpurun_out/abbuild.log; exit 3; }
 cp cudaraytracer_amd/librt_hip.so /tmp/ablib/product.so
 one() {  # lib label args
