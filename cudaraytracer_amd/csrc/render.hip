@@ -2167,6 +2167,10 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
     // A path ended with `contrib` (Kernel.cu:147): the next sample's camera ray (Kernel.cu:139-146), or done.  With
     // max_depth = 0 every sample is black but still draws its camera jitter (Kernel.cu:79).
     const auto next_sample = [&](const f3 contrib) {
+        // (COUNT_TESTS: counted on the call's lowest active lane, summed over all lanes at the end)
+        const uint64_t c0 = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t lead = COUNT_TESTS ? wave_leader() : 0u;
+        if (COUNT_TESTS) cnt.idle_wait += lead * (uint32_t)__popcll(__ballot(1));
         col = add(col, contrib);
         KParamsC* q = kparams_reload();
         const Camera cam = lane_camera(q, x, g);
@@ -2181,6 +2185,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
             col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
         }
         mode = MODE_DONE;
+        if (COUNT_TESTS) cnt.wleaf += lead * (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     };
     if (P.spp > 0) next_sample(mk(0.0f, 0.0f, 0.0f));  // (col + 0 = +0)
 
@@ -2189,12 +2194,24 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
     int hit = -1;
     uint32_t tag = 0u;
     float t = FLT_MAX;
+    // COUNT_TESTS (tools/flat_phases.py): wave cycles in the trace (ctrav) / shading, camera rays included (cshade) /
+    // camera-ray code (wleaf), passes (wnode), and per pass the lanes tracing (idle_nt), shading (idle_fin) and
+    // starting a sample (idle_wait)
     while (__ballot(mode != MODE_DONE) != 0) {
+        const uint64_t c0 = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        if (COUNT_TESTS) {
+            const uint32_t lead = wave_leader();
+            cnt.wnode += lead;
+            cnt.idle_nt += lead * (uint32_t)__popcll(__ballot(mode == MODE_TRAV));
+            cnt.idle_fin += lead * (uint32_t)__popcll(__ballot(mode == MODE_TRAV || mode == MODE_SHADE));
+        }
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
             flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.flat_boxes, P.num_prims, ro, rd, hit, tag, t, cnt);
             mode = MODE_SHADE;
         }
+        const uint64_t c1 = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
+        if (COUNT_TESTS) cnt.ctrav += c1 - c0;
         if (mode == MODE_SHADE) {
             if (COUNT_TESTS) cnt.wshade += wave_leader();
             f3 contrib;
@@ -2206,7 +2223,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
                 else mode = MODE_TRAV;
             }
         }
+        if (COUNT_TESTS) cnt.cshade += __builtin_amdgcn_s_memtime() - c1;
     }
+    if (COUNT_TESTS) cnt.ctotal = __builtin_amdgcn_s_memtime() - w_start;
     if (P.wave_trace && wave_leader() && 2ull * tile + 2ull <= P.wave_trace_words) {
         P.wave_trace[2 * tile] = rt_start;
         P.wave_trace[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();

@@ -577,6 +577,37 @@ def _small_rects_scene():
     return scenes.Scene(h, m, [])
 
 
+@pytest.mark.parametrize("rng", ["xorwow", "philox"])
+@pytest.mark.parametrize("variant", [5, 6])
+def test_flat_kernels_exact_on_ties_and_box_faces(variant, rng):
+    """The flat kernels' exactness argument (render.hip flat_trace: a geometric closest hit is the reference's unless
+    it ties, lies within rounding of a face of its own reference box, or a NaN took part — those rays replay the
+    reference BVH) on a scene built to hit every case: coplanar rectangles that overlap (exact ties in t over an
+    area) and abut (shared edges), a floor and a wall meeting their edges, spheres tangent to the rectangles'
+    plane and touching the floor and wall with their box faces, a mirror sphere for reflected rays.  In this scene the
+    reference's box culling changes 521 pixels against the brute-force closest hit (tests/test_scene_adversarial.py
+    pins that on the CPU), so the whole frame, the RNG states and the ray count must equal the oracle's reference
+    traversal, not the geometric answer."""
+    from adversarial_scene import ADVERSARIAL_CONFIG, adversarial_scene
+    cfg, sc = ADVERSARIAL_CONFIG, adversarial_scene()
+    lib().rt_set_variant(variant)
+    r = Renderer(cfg.width, cfg.height, rng=rng)
+    r.render_init()
+    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), frame=3)
+    torch.cuda.synchronize()
+    assert lib().rt_last_variant() == variant
+    philox = rng == "philox"
+    st = None if philox else po.init_states(cfg.width, cfg.height)
+    ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                            philox=philox, seed=1984, frame=3)
+    img = r.image()
+    bad = np.argwhere(img != ref)
+    assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
+    if not philox:
+        np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
+    assert int(r.counters[0]) == cnt.rays
+
+
 @pytest.mark.parametrize("variant", KEY_VARIANTS + [0, 1])
 def test_far_camera_small_primitives_match_brute_force(variant):
     """Box culling stays conservative far from the scene (the slab test's rounding grows with the
