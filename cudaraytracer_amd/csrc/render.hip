@@ -2991,7 +2991,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     int trial_slot = 0;
     const bool automatic = variant < 0 || variant >= kNumVariants;
     // small scenes: the flat kernel takes v3's place (in the trial below 64 spp as well)
-    const bool flat_ok = S.prims_flat && S.num_prims <= (uint32_t)g_flat_max;
+    // (and up to kFlatMaxPrims primitives when rectangles touch other primitives: the flat kernels are exact there,
+    // the BVH kernels return the geometric closest hit, tests/adversarial_scene.py)
+    const bool flat_ok = S.prims_flat && (S.num_prims <= (uint32_t)g_flat_max || (S.touching_rects && g_flat_max > 0));
     const int tile_kernel = flat_ok ? kVarFlat : kVarV3Compact;
     const int persistent_kernel = flat_ok ? kVarFlatPersistent : kVarV4;
     if (automatic) {

@@ -74,6 +74,9 @@ struct HostScene {
     std::vector<float> ref_nodes;      // ... and the reference BVH itself: 8 floats per node (scene_build.cpp)
     std::vector<float> flat_boxes;     // ... and per flat record its reference box for the flat kernels' exactness
                                        // check: 8 floats (scene_build.cpp)
+    bool touching_rects = false;       // a rectangle's reference box touches or overlaps another primitive's: rays
+                                       // there can tie or graze a box face (the automatic choice keeps such scenes
+                                       // of <= kFlatMaxPrims primitives on the exact flat kernels)
 };
 
 // Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.  with_texels = false computes

@@ -576,6 +576,20 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
             std::vector<int> ord;
             reference_test_order(rn, 0, &ord);
             std::vector<int> flat_index(desc->num_hittables, -1);
+            // a rectangle whose reference box touches or overlaps another primitive's (closed intervals on every
+            // axis): coplanar or abutting rectangles, walls meeting, a sphere resting on a floor
+            std::vector<std::array<float, 6>> boxes(ord.size());
+            for (size_t i = 0; i < ord.size(); i++) ref_prim_box(desc->hittables[ord[i]], boxes[i].data(), boxes[i].data() + 3);
+            for (size_t i = 0; i < ord.size() && !out->touching_rects; i++) {
+                if (desc->hittables[ord[i]].type == RT_SPHERE) continue;
+                for (size_t j = 0; j < ord.size() && !out->touching_rects; j++) {
+                    if (j == i) continue;
+                    bool touch = true;
+                    for (int a = 0; a < 3; a++)
+                        touch = touch && boxes[i][a] <= boxes[j][3 + a] && boxes[j][a] <= boxes[i][3 + a];
+                    out->touching_rects = touch;
+                }
+            }
             out->prims_flat.resize(ord.size() * 8);
             out->flat_boxes.resize(ord.size() * 8);
             for (size_t i = 0; i < ord.size(); i++) {

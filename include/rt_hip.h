@@ -328,11 +328,15 @@ int rt_last_variant(void);
  *   RT_TUNE_LEAF_BREAK: the v3 kernels leave the node-visit loop for the leaf tests once at most this many of
  *   the still-traversing lanes hold no leaf (0..64, default 3; 0 = once every lane holds one).  Nor does this.
  *   RT_TUNE_FLAT_MAX: scenes of at most this many active primitives (0..64, default 16) run the flat kernels
- *   (variants 5 and 6: no BVH, every ray tests every primitive in the reference BVH's test order) where the
- *   automatic choice would run variant 3 or 4.  RT_TUNE_RIUS_TRIPS: the flat kernels make at most this many
- *   RandomInUnitSphere attempts (Math.cuh:252-260) per shading pass; a lane whose attempts were all rejected
- *   continues the same call at the wave's next pass (0 = unbounded; 0..64; default 4; Philox mode rounds it up
- *   to whole blocks of four attempts).  Neither changes the image. */
+ *   (variants 5 and 6: no BVH, every ray tests every primitive in the reference BVH's test order, and rays whose
+ *   answer the reference's box culling could change replay the reference BVH: the reference's pixels for any
+ *   geometry) where the automatic choice would run variant 3 or 4; so do scenes of up to 64 primitives in which a
+ *   rectangle's reference box touches another primitive's (coplanar, abutting or meeting rectangles, a sphere on a
+ *   floor), unless the value is 0.  The BVH kernels return the geometric closest hit, which differs from the
+ *   reference's only on exact ties and hits within rounding of a reference box face.  RT_TUNE_RIUS_TRIPS: the flat
+ *   kernels make at most this many RandomInUnitSphere attempts (Math.cuh:252-260) per shading pass; a lane whose
+ *   attempts were all rejected continues the same call at the wave's next pass (0 = unbounded; 0..64; default 4;
+ *   Philox mode rounds it up to whole blocks of four attempts).  It does not change the image. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,

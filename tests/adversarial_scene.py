@@ -41,3 +41,18 @@ def adversarial_scene() -> scenes.Scene:
         m[k].albedo.type, m[k].albedo.image = abi.RT_CONSTANT, -1
         m[k].albedo.color[:] = list(col)
     return scenes.Scene(h, m, [])
+
+
+def adversarial_scene_large(extra: int = 12) -> scenes.Scene:
+    """The adversarial scene plus `extra` small Lambertian spheres floating above it (17+ primitives: beyond the flat
+    kernels' size limit, kept on them by the touching rectangles)."""
+    base = adversarial_scene()
+    n = len(base.hittables) + extra
+    h = (abi.HittableDesc * n)()
+    for i in range(len(base.hittables)):
+        h[i] = base.hittables[i]
+    for k in range(extra):
+        i = len(base.hittables) + k
+        h[i].type, h[i].is_active, h[i].material, h[i].radius = abi.RT_SPHERE, 1, k % 5, 0.15
+        h[i].center[:] = [-1.8 + 0.35 * k, 1.6 + 0.1 * (k % 3), 0.8 + 0.2 * (k % 4)]
+    return scenes.Scene(h, base.materials, [])

@@ -608,6 +608,37 @@ def test_flat_kernels_exact_on_ties_and_box_faces(variant, rng):
     assert int(r.counters[0]) == cnt.rays
 
 
+@pytest.mark.parametrize("spp", [4, 64])
+def test_touching_rectangles_keep_larger_scenes_on_the_exact_kernels(spp):
+    """A scene beyond RT_TUNE_FLAT_MAX (20 primitives) whose rectangles touch (the adversarial scene plus 12 spheres):
+    the automatic choice keeps it on the flat kernels (both sides of the spp rule: the persistent one below 64 spp
+    after its trial, the tile one from 64), so the whole frame is the reference's; the 17-primitive startup world,
+    whose one rectangle touches nothing, stays on the BVH kernels."""
+    from adversarial_scene import ADVERSARIAL_CONFIG, adversarial_scene_large
+    cfg = ADVERSARIAL_CONFIG.scaled(ADVERSARIAL_CONFIG.width, ADVERSARIAL_CONFIG.height, spp)
+    sc = adversarial_scene_large()
+    assert len(sc.hittables) == 20
+    ds = DeviceScene(sc)
+    lib().rt_set_variant(-1)
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    frames = 4 if spp < 64 else 1  # below 64 spp: the automatic choice's trial frames, then the chosen kernel
+    st = po.init_states(cfg.width, cfg.height)
+    for _ in range(frames):
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+        torch.cuda.synchronize()
+        assert lib().rt_last_variant() in (5, 6)
+        ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
+        np.testing.assert_array_equal(r.image(), ref)
+    np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
+    dw = scenes.CONFIGS["default"]
+    r2 = Renderer(64, 48)
+    r2.render_init()
+    r2.render(DeviceScene(scenes.builtin(dw.scene)), 64, 4, dw.inputs())
+    torch.cuda.synchronize()
+    assert lib().rt_last_variant() in (2, 3)
+
+
 @pytest.mark.parametrize("variant", KEY_VARIANTS + [0, 1])
 def test_far_camera_small_primitives_match_brute_force(variant):
     """Box culling stays conservative far from the scene (the slab test's rounding grows with the
