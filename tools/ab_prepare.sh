@@ -12,6 +12,6 @@ if ! git -C "$ROOT" rev-parse --verify -q "$rev^{commit}" > /dev/null; then
   exit 2
 fi
 rm -rf "$out"; mkdir -p "$out"
-git -C "$ROOT" archive "$rev" cudaraytracer_amd include | tar -x -C "$out"
-if [ -n "$patch" ]; then (cd "$out" && git apply --include='cudaraytracer_amd/*' --include='include/*' "$ROOT/$patch"); fi
+git -C "$ROOT" archive "$rev" cudaraytracer_amd include tests | tar -x -C "$out"
+if [ -n "$patch" ]; then patch -d "$out" -p1 --forward --quiet < "$ROOT/$patch" || { echo "ab_prepare: $patch does not apply to $rev" >&2; exit 3; }; grep -q . "$ROOT/$patch" || exit 3; fi
 echo "ab_prepare: $out = $rev${patch:+ + $patch}"
