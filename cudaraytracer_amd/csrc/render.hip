@@ -501,7 +501,8 @@ struct Camera {
 
 // Camera ray of one sample (Kernel.cu:139-146): two uniforms, then the reference's plane construction.
 template <class PP, class R>
-__device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& ro, f3& rd) {
+__device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& ro, f3& rd, uint32_t sample) {
+    begin_sample(rng, sample);  // (Philox mode: the sample's own window of the pixel's stream)
     float xi1, xi2;
     draw2(rng, xi1, xi2);
     // (x - cx + ξ) / width: the dividend is +0 or at least 2^-33 in magnitude (ξ in (0, 1]), inside div_rn's range
@@ -680,6 +681,7 @@ template <class R>
 __device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32_t* st, const R& rng, f3 col,
                                             const float4* acc_pre = nullptr) {
     store_rng(P, st, rng);
+    col = pixel_sum(rng, col);
     f3 c;
     if (P.flags & RT_FLAG_ACCUMULATE) {
         float4 a = acc_pre ? *acc_pre : P.accum[pix];  // (acc_pre: the value loaded when the pixel started)
@@ -811,6 +813,35 @@ struct RngPhilox {
     uint32_t n, r0, r1, r2, r3, pix;  // n: the next group's block; r0..r3: the current block (not carried)
     uint32_t k0, k1, frame;  // launch-uniform key and frame, read once when the stream is (un)parked
 };
+
+// Per-sample RNG window and pixel sum.  XORWOW (the reference's mode): one sequential stream per pixel, samples
+// summed in float in order (Kernel.cu:147).  Philox mode: sample s starts at block s << 16 of the pixel's stream
+// (rocrand_init(seed, pixel, (frame << 34) + (s << 18))), and the samples are summed in 2^-12 fixed point,
+// saturating (the float registers carry the uint32 sums) — so neither the draws nor the sum depend on the order the
+// samples run in (oracle/rt_oracle.c orc_quant, the same operations).
+__device__ __forceinline__ void begin_sample(Rng&, uint32_t) {}
+__device__ __forceinline__ void begin_sample(RngPhilox& s, uint32_t sample) { s.n = sample << 16; }
+__device__ __forceinline__ uint32_t quant12(const float x) {  // NaN, <= 0: 0; >= 2^20 - 1: saturated
+    if (!(x > 0.0f)) return 0u;
+    if (!(x < 1048575.0f)) return 0xffffffffu;
+    return (uint32_t)(x * 4096.0f + 0.5f);  // (x · 4096 exact: one rounding, the + 0.5's)
+}
+__device__ __forceinline__ uint32_t sat_add(const uint32_t a, const uint32_t b) {
+    const uint32_t t = a + b;
+    return t < b ? 0xffffffffu : t;
+}
+__device__ __forceinline__ f3 add_sample(const Rng&, const f3 col, const f3 c) { return add(col, c); }
+__device__ __forceinline__ f3 add_sample(const RngPhilox&, const f3 col, const f3 c) {
+    return mk(__uint_as_float(sat_add(__float_as_uint(col.x), quant12(c.x))),
+              __uint_as_float(sat_add(__float_as_uint(col.y), quant12(c.y))),
+              __uint_as_float(sat_add(__float_as_uint(col.z), quant12(c.z))));
+}
+__device__ __forceinline__ f3 pixel_sum(const Rng&, const f3 col) { return col; }
+__device__ __forceinline__ f3 pixel_sum(const RngPhilox&, const f3 col) {
+    return mk((float)__float_as_uint(col.x) * (1.0f / 4096.0f), (float)__float_as_uint(col.y) * (1.0f / 4096.0f),
+              (float)__float_as_uint(col.z) * (1.0f / 4096.0f));
+}
+
 
 // Block `blk` of the lane's stream: philox10(ctr = {blk, frame, pixel, 0}, key = seed) into s.r0..r3.
 // The key and frame are re-read from the kernel arguments here (scalar loads) rather than carried: held across
@@ -960,7 +991,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
     if (P.spp > 0) {
         while (true) {
             if (need_camera) {
-                camera_ray(&P, cam, rng, ro, rd);
+                camera_ray(&P, cam, rng, ro, rd, sample);
                 att = mk(1.0f, 1.0f, 1.0f);
                 depth = 0;
                 need_camera = false;
@@ -980,7 +1011,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
                 if (!done) depth++;
             }
             if (done) {
-                col = add(col, contrib);
+                col = add_sample(rng, col, contrib);
                 if (++sample == P.spp) break;
                 need_camera = true;
             }
@@ -1002,6 +1033,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
 // ---------------------------------------------------------------------------------------------------
 constexpr int kSentinel = 0x7fffffff;  // traversal finished (internal node ids are < it, leaves < 0)
 enum LaneMode { MODE_TRAV = 0, MODE_SHADE = 1, MODE_DONE = 2 };
+constexpr int MODE_NEED = 3;  // v4 / persistent flat: the lane waits for a pixel; v3 sample items: for a sample
 
 template <bool COUNT_TESTS, int BLOCK = 64>
 __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
@@ -1046,9 +1078,9 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
     };
     // A path ended with `contrib`: accumulate (Kernel.cu:147) and begin the next sample, or finish.
     auto next_sample = [&](f3 contrib) {
-        col = add(col, contrib);
+        col = add_sample(rng, col, contrib);
         while (++sample < P.spp) {
-            camera_ray(&P, cam, rng, ro, rd);
+            camera_ray(&P, cam, rng, ro, rd, sample);
             att = mk(1.0f, 1.0f, 1.0f);
             depth = 0;
             cnt.primary++;
@@ -1056,7 +1088,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
                 start_trace();
                 return;
             }
-            col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+            col = add_sample(rng, col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
         }
         mode = MODE_DONE;
     };
@@ -1243,18 +1275,18 @@ template <bool WIDE, class R>
 __device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uint32_t g, f3 contrib, R& rng,
                                                f3& col, f3& att, uint32_t& sample, uint32_t& depth, f3& ro,
                                                f3& rd, Cursor& c, uint32_t& rays) {
-    col = add(col, contrib);
+    col = add_sample(rng, col, contrib);
     KParamsC* q = kparams_reload();
     const Camera cam = lane_camera(q, x, g);
     while (++sample < P.spp) {
-        camera_ray(q, cam, rng, ro, rd);
+        camera_ray(q, cam, rng, ro, rd, sample);
         att = mk(1.0f, 1.0f, 1.0f);
         depth = 0;
         if (P.max_depth > 0) {
             v3_start_trace<WIDE>(P.num_nodes, c, rays);
             return;
         }
-        col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+        col = add_sample(rng, col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
     }
     c.mode = MODE_DONE;
 }
@@ -1657,6 +1689,21 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
     Cursor c{(int)RefW<WIDE>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_DONE};
 
+    // Sample items (Philox mode, compact parking: the default Philox kernel; full tiles).  Philox draws and sums do not
+    // depend on the order a pixel's samples run in (begin_sample, add_sample), so the tile's 64 × spp samples are work
+    // items that whichever lane's path has ended takes next — no lane idles because its own pixel is done while the
+    // wave's slowest pixel still renders (7 of 64 lanes per node iteration on C2).  Item i is sample i / 64 of pixel
+    // i % 64 (the tile's pixels in lane order, sample-major: a wave's lanes stay on one tile); a path's sample goes
+    // into its pixel's 64-bit fixed-point sums in LDS — parking words 1-4 (R, G) and 6-7 (B), which the Philox stream
+    // (words 0, 5) and this mode's parking (no colour words) leave free; word 8 counts the lane's finished paths' rays
+    // (the packed 13-bit ray field holds one path's); the packed sample field holds the item's pixel.
+    constexpr bool kItemsBuild = PHILOX && COMPACT;
+    const bool items = kItemsBuild && P.spp > 0 && P.max_depth > 0 && __ballot(1) == ~0ull;  // (wave-uniform)
+    uint32_t next_item = 64u;  // wave-uniform: items 0-63 (every pixel's sample 0) start below
+    const uint32_t n_items = P.spp * 64u;
+    const auto item_sum = [&](uint32_t p, int ch) -> unsigned long long* {
+        return (unsigned long long*)(wl + (ch < 2 ? 64u + 2u * ((uint32_t)ch * 64u + p) : 384u + 2u * p));
+    };
     {  // first camera ray of the pixel
         uint32_t* st = state_at(P, pix);
         R rng = begin_rng<R>(st, P.state_stride, g * P.width + x);  // global pixel index (Kernel.cu:119)
@@ -1665,7 +1712,11 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         // sample field cannot spill into the ray count)
         uint32_t sample = P.spp > 0 ? (uint32_t)-1 : 0u, depth = 0, rays = 0;
         if (P.spp > 0) v3_next_sample<WIDE>(P, x, g, mk(0.0f, 0.0f, 0.0f), rng, col, att, sample, depth, ro, rd, c, rays);
-        v3_park<COMPACT>(park, rng, col, att, sample, depth, rays);  // (col + 0 = +0 above)
+        v3_park<COMPACT>(park, rng, col, att, items ? lane : sample, depth, rays);  // (col + 0 = +0 above)
+        if (kItemsBuild && items) {  // (after the park above, which wrote colour words)
+            park[1 * 64] = park[2 * 64] = park[3 * 64] = park[4 * 64] = 0u;
+            park[6 * 64] = park[7 * 64] = park[8 * 64] = 0u;
+        }
     }
     const uint32_t threshold = P.regen_threshold;
 
@@ -1695,7 +1746,15 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
-            if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
+            if (kItemsBuild && items && ended) {  // this sample into its pixel's sums; the lane takes the next item below
+                const uint32_t q0 = quant12(contrib.x), q1 = quant12(contrib.y), q2 = quant12(contrib.z);
+                if (q0) atomicAdd(item_sum(sample, 0), (unsigned long long)q0);
+                if (q1) atomicAdd(item_sum(sample, 1), (unsigned long long)q1);
+                if (q2) atomicAdd(item_sum(sample, 2), (unsigned long long)q2);
+                park[8 * 64] += rays;
+                rays = 0u;
+                c.mode = MODE_NEED;
+            } else if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
                 col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
                          __uint_as_float(park[(PK_COL + 2) * 64]));
                 v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
@@ -1706,6 +1765,30 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
                 v3_start_trace<WIDE>(P.num_nodes, c, rays);
             }
             v3_park<COMPACT, false>(park, rng, col, att, sample, depth, rays);
+        }
+        if constexpr (kItemsBuild) {
+            // lanes whose path ended take the next items (ballot + mbcnt rank on the wave-uniform counter)
+            const uint64_t needm = __ballot(c.mode == MODE_NEED);
+            if (items && needm != 0) {
+                const uint32_t item = next_item +
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+                next_item += (uint32_t)__popcll(needm);
+                if (c.mode == MODE_NEED) {
+                    if (item < n_items) {
+                        const uint32_t p = item & 63u;
+                        const uint32_t bx = tile % P.tiles_x, by = tile / P.tiles_x;
+                        const uint32_t px = bx * 8u + (p & 7u), pg = global_row(P, by * 8u + (p >> 3));
+                        R rng = begin_rng<R>(nullptr, 0u, pg * P.width + px);
+                        KParamsC* q = kparams_reload();
+                        camera_ray(q, lane_camera(q, px, pg), rng, ro, rd, item >> 6);
+                        uint32_t rays = 0u;
+                        v3_start_trace<WIDE>(P.num_nodes, c, rays);
+                        v3_park<COMPACT, false>(park, rng, mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), p, 0u, rays);
+                    } else {
+                        c.mode = MODE_DONE;
+                    }
+                }
+            }
         }
         if (COUNT_TESTS) cnt.cshade += __builtin_amdgcn_s_memtime() - t_b;
         if (__ballot(c.mode != MODE_DONE) == 0) break;
@@ -1723,6 +1806,11 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     f3 col, att;
     uint32_t sample, depth, rays;
     v3_unpark<COMPACT>(park, rng, col, att, sample, depth, rays);
+    if (kItemsBuild && items) {  // this lane's pixel's sums (every lane's adds are done: LDS keeps a wave's order)
+        const auto sat = [](unsigned long long v) { return __uint_as_float(v > 0xffffffffull ? 0xffffffffu : (uint32_t)v); };
+        col = mk(sat(*item_sum(lane, 0)), sat(*item_sum(lane, 1)), sat(*item_sum(lane, 2)));
+        rays += park[8 * 64];
+    }
     cnt.rays = rays;
     cnt.primary = P.spp;  // every sample starts with one camera ray (Kernel.cu:137-146)
     finish_pixel<COUNT_TESTS>(P, pix, state_at(P, pix), rng, col, cnt);
@@ -1743,7 +1831,6 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
 // LDS per wave: 18 × 256 B of parked state + (depth + 2) × 128 B of stack.
 // ---------------------------------------------------------------------------------------------------
 enum ParkSlotV4 { PK_X = PK_WORDS, PK_G = PK_WORDS + 1, PK_PIX = PK_WORDS + 2, PK_WORDS4 = PK_WORDS + 3 };
-constexpr int MODE_NEED = 3;  // v4: lane waits for a pixel
 
 // Work index → pixel of the local image (8×8 tiles, row-major tile order); false when the index lies
 // outside the image or outside the rendered grid.
@@ -1869,7 +1956,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
             if (ended) {
-                col = add(col, contrib);  // Kernel.cu:147
+                col = add_sample(rng, col, contrib);  // Kernel.cu:147
                 if (++sample < P.spp) {
                     cam = true;
                 } else {  // the pixel is done (Kernel.cu:149-157)
@@ -1899,7 +1986,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
         if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
             KParamsC* q = kparams_reload();
             const Camera cam_l = lane_camera(q, park[PK_X * 64], park[PK_G * 64]);
-            camera_ray(q, cam_l, rng, ro, rd);
+            camera_ray(q, cam_l, rng, ro, rd, sample);
             att = mk(1.0f, 1.0f, 1.0f);
             depth = 0u;
             v3_start_trace<WIDE>(P.num_nodes, c, rays);
@@ -2171,18 +2258,18 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
         const uint64_t c0 = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t lead = COUNT_TESTS ? wave_leader() : 0u;
         if (COUNT_TESTS) cnt.idle_wait += lead * (uint32_t)__popcll(__ballot(1));
-        col = add(col, contrib);
+        col = add_sample(rng, col, contrib);
         KParamsC* q = kparams_reload();
         const Camera cam = lane_camera(q, x, g);
         while (++sample < P.spp) {
-            camera_ray(q, cam, rng, ro, rd);
+            camera_ray(q, cam, rng, ro, rd, sample);
             att = mk(1.0f, 1.0f, 1.0f);
             depth = 0u;
             if (P.max_depth > 0u) {
                 mode = MODE_TRAV;
                 return;
             }
-            col = add(col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
+            col = add_sample(rng, col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
         }
         mode = MODE_DONE;
         if (COUNT_TESTS) cnt.wleaf += lead * (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
@@ -2291,7 +2378,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
             if (ended) {
-                col = add(col, contrib);  // Kernel.cu:147
+                col = add_sample(rng, col, contrib);  // Kernel.cu:147
                 if (++sample < P.spp) {
                     cam = true;
                 } else {  // the pixel is done (Kernel.cu:149-157)
@@ -2341,7 +2428,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
         }
         if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
             KParamsC* q = kparams_reload();
-            camera_ray(q, lane_camera(q, x, g), rng, ro, rd);
+            camera_ray(q, lane_camera(q, x, g), rng, ro, rd, sample);
             att = mk(1.0f, 1.0f, 1.0f);
             depth = 0u;
             mode = MODE_TRAV;

@@ -122,7 +122,10 @@ float orc_curand_uniform(rt_curand_state* s) {
 /* lo, seed hi}) (rocrand_uniform4) in draw groups that start on a block boundary: the camera       */
 /* jitter (Kernel.cu:139-140) and the dielectric's choice (Material.cuh:131) one group each, a      */
 /* whole RandomInUnitSphere call (Math.cuh:252-260, 3 draws per attempt) one group (the kernel's   */
-/* RngPhilox, render.hip).  Pinned by tests/golden/philox_kat.json (rocRAND's own engine).         */
+/* RngPhilox, render.hip).  Sample s of a pixel starts at block s << 16 (its own window of 2^16     */
+/* blocks: offset (frame << 34) + (s << 18)), and the pixel's samples are summed in 2^-12 fixed      */
+/* point (orc_quant), so neither depends on the order the samples run in.  Pinned by                */
+/* tests/golden/philox_kat.json (rocRAND's own engine).                                              */
 /* ---------------------------------------------------------------------------------------------- */
 void orc_philox4x32_10(const unsigned int ctr_in[4], const unsigned int key_in[2], unsigned int out[4]) {
     unsigned int c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
@@ -145,6 +148,18 @@ void orc_philox4x32_10(const unsigned int ctr_in[4], const unsigned int key_in[2
 /* uniform in (0, 1]: 2^-32 + x·2^-32 (rocrand_uniform.h:65-68).  x·2^-32 is exact, so a fused and an
  * unfused evaluation agree. */
 static inline float philox_to_uniform(unsigned int x) { return 2.3283064e-10f + (float)x * 2.3283064e-10f; }
+
+/* Philox mode's per-sample contribution in 2^-12 fixed point: NaN, negative and zero give 0, values from 2^20 - 1
+ * on saturate; x · 4096 is exact, so the one rounding is the + 0.5's; the sum saturates at 2^32 - 1. */
+static inline unsigned orc_quant(float x) {
+    if (!(x > 0.0f)) return 0u;
+    if (!(x < 1048575.0f)) return 0xffffffffu;
+    return (unsigned)(x * 4096.0f + 0.5f);
+}
+static inline unsigned orc_sat_add(unsigned a, unsigned b) {
+    unsigned s = a + b;
+    return s < b ? 0xffffffffu : s;
+}
 
 float orc_philox_uniform_at(unsigned long long seed, unsigned int pixel, unsigned int frame, unsigned int n) {
     unsigned int ctr[4] = {n >> 2, frame, pixel, 0u};
@@ -715,7 +730,9 @@ void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, float* a
                 g.xs = &st;
             }
             v3 col = mk(0.0f, 0.0f, 0.0f);
+            unsigned q[3] = {0u, 0u, 0u}; /* Philox: the fixed-point sum */
             for (unsigned smp = 0; smp < spp; smp++) {
+                if (philox) g.n = smp << 18; /* the sample's own window: block smp << 16 */
                 orc_group(&g);
                 float u = ((float)((float)x - center.x) + orc_uniform(&g)) / (float)width;
                 float v = ((float)(center.y - (float)y) + orc_uniform(&g)) / (float)width;
@@ -724,8 +741,16 @@ void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, float* a
                 v3 second = add(add(scale(in->far_plane, dist), scale(1.0f / in->fov * 10.0f, fwd)), origin);
                 v3 dir = normalize(sub(second, start));
                 c.primary++;
-                col = add(col, color(s, start, dir, (int)max_depth, &g, in, order, &c));
+                v3 cs = color(s, start, dir, (int)max_depth, &g, in, order, &c);
+                if (philox) {
+                    q[0] = orc_sat_add(q[0], orc_quant(cs.x));
+                    q[1] = orc_sat_add(q[1], orc_quant(cs.y));
+                    q[2] = orc_sat_add(q[2], orc_quant(cs.z));
+                } else {
+                    col = add(col, cs);
+                }
             }
+            if (philox) col = mk((float)q[0] * (1.0f / 4096.0f), (float)q[1] * (1.0f / 4096.0f), (float)q[2] * (1.0f / 4096.0f));
             if (!philox) state[pixel_index] = st;
             if (accum) { /* progressive accumulation (not in the reference): running sum of
                             samples and sample count per pixel, the image shows their quotient */
