@@ -2275,6 +2275,24 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
         if (COUNT_TESTS) cnt.wleaf += lead * (uint32_t)(__builtin_amdgcn_s_memtime() - c0);
     };
     if (P.spp > 0) next_sample(mk(0.0f, 0.0f, 0.0f));  // (col + 0 = +0)
+    // Sample items (Philox mode, full tiles; as render_kernel_v3): a path that ends puts its sample into its pixel's
+    // 64-bit fixed-point sums in LDS, and the lane takes the tile's next sample item (i: sample i / 64 of pixel i % 64)
+    constexpr bool kItemsBuild = PHILOX;
+    __shared__ unsigned long long item_sums[kItemsBuild ? 192 : 1];  // R, G, B x 64 pixels
+    const bool items = kItemsBuild && P.spp > 0 && P.max_depth > 0 && __ballot(1) == ~0ull;  // (wave-uniform)
+    uint32_t next_item = 64u, item_p = threadIdx.x & 63u;
+    if (kItemsBuild && items) item_sums[item_p] = item_sums[64u + item_p] = item_sums[128u + item_p] = 0ull;
+    const auto end_path = [&](const f3 contrib) {
+        if (kItemsBuild && items) {
+            const uint32_t q0 = quant12(contrib.x), q1 = quant12(contrib.y), q2 = quant12(contrib.z);
+            if (q0) atomicAdd(&item_sums[item_p], (unsigned long long)q0);
+            if (q1) atomicAdd(&item_sums[64u + item_p], (unsigned long long)q1);
+            if (q2) atomicAdd(&item_sums[128u + item_p], (unsigned long long)q2);
+            mode = MODE_NEED;
+        } else {
+            next_sample(contrib);
+        }
+    };
 
     const uint64_t w_start = __builtin_amdgcn_s_memtime();
     const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
@@ -2304,13 +2322,41 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
             f3 contrib;
             const int res = shade<TEX, true>(kparams_reload(), prims, hit, tag, t, ro, rd, att, rng, rtl, contrib);
             if (res == SHADE_ENDED) {
-                next_sample(contrib);
+                end_path(contrib);
             } else if (res == SHADE_CONTINUE) {
-                if (++depth >= P.max_depth) next_sample(mk(0.0f, 0.0f, 0.0f));  // Kernel.cu:79
+                if (++depth >= P.max_depth) end_path(mk(0.0f, 0.0f, 0.0f));  // Kernel.cu:79
                 else mode = MODE_TRAV;
             }
         }
+        if constexpr (kItemsBuild) {  // lanes whose path ended take the next items (as render_kernel_v3)
+            const uint64_t needm = __ballot(mode == MODE_NEED);
+            if (items && needm != 0) {
+                const uint32_t item = next_item +
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+                next_item += (uint32_t)__popcll(needm);
+                if (mode == MODE_NEED) {
+                    if (item < P.spp * 64u) {
+                        item_p = item & 63u;
+                        const uint32_t bx = tile % P.tiles_x, by = tile / P.tiles_x;
+                        const uint32_t px = bx * 8u + (item_p & 7u), pg = global_row(P, by * 8u + (item_p >> 3));
+                        rng = begin_rng<R>(nullptr, 0u, pg * P.width + px);
+                        KParamsC* q = kparams_reload();
+                        camera_ray(q, lane_camera(q, px, pg), rng, ro, rd, item >> 6);
+                        att = mk(1.0f, 1.0f, 1.0f);
+                        depth = 0u;
+                        mode = MODE_TRAV;
+                    } else {
+                        mode = MODE_DONE;
+                    }
+                }
+            }
+        }
         if (COUNT_TESTS) cnt.cshade += __builtin_amdgcn_s_memtime() - c1;
+    }
+    if (kItemsBuild && items) {  // this lane's pixel's sums (every lane's adds are done: LDS keeps a wave's order)
+        const auto sat = [](unsigned long long v) { return __uint_as_float(v > 0xffffffffull ? 0xffffffffu : (uint32_t)v); };
+        const uint32_t l = threadIdx.x & 63u;
+        col = mk(sat(item_sums[l]), sat(item_sums[64u + l]), sat(item_sums[128u + l]));
     }
     if (COUNT_TESTS) cnt.ctotal = __builtin_amdgcn_s_memtime() - w_start;
     if (P.wave_trace && wave_leader() && 2ull * tile + 2ull <= P.wave_trace_words) {

@@ -232,14 +232,18 @@ enum rt_render_flags {
                                              unspecified and nvcc's is not established).
                                              Both orders are tested against the oracle on every config. */
     RT_FLAG_COUNT_TESTS = 1u << 4, /* also count box and primitive tests into counters[1], [2] */
-    RT_FLAG_RNG_PHILOX = 1u << 5,  /* perf-mode RNG: each pixel draws from the hipRAND/rocRAND Philox4x32-10
-                                      stream rocrand_init(rng_seed, subsequence = global pixel index,
-                                      offset = rng_frame << 34), read as rocrand_uniform4 blocks in draw
-                                      groups that start on a block boundary (the camera jitter, the
-                                      dielectric's choice, a whole RandomInUnitSphere call), instead of
-                                      its cuRAND XORWOW state.  `state` is neither read nor written (may be NULL): no
-                                      per-pixel RNG bytes in HBM.  Not the reference's stream (its images
-                                      match the parity mode statistically, not bit for bit). */
+    RT_FLAG_RNG_PHILOX = 1u << 5,  /* perf-mode RNG: sample s of a pixel draws from the hipRAND/rocRAND
+                                      Philox4x32-10 stream rocrand_init(rng_seed, subsequence = global pixel
+                                      index, offset = (rng_frame << 34) + (s << 18)), read as rocrand_uniform4
+                                      blocks in draw groups that start on a block boundary (the camera jitter,
+                                      the dielectric's choice, a whole RandomInUnitSphere call), instead of its
+                                      cuRAND XORWOW state; the pixel's samples are summed in 2^-12 fixed point
+                                      (each sample's channel rounded to the nearest multiple of 2^-12, the sum
+                                      saturating at 2^20), so neither the draws nor the sum depend on the order
+                                      the samples run in — the kernels hand a tile's samples to whichever lane
+                                      is free.  `state` is neither read nor written (may be NULL): no per-pixel
+                                      RNG bytes in HBM.  Not the reference's stream (its images match the parity
+                                      mode statistically, not bit for bit). */
     RT_FLAG_STATE_SOA = 1u << 6    /* `state` holds the XORWOW states as six uint32 planes (rt_render_init_soa)
                                       instead of rt_curand_state structs: the same streams and images, 24 B
                                       per pixel read and written with coalesced 4-B accesses (the 48-B

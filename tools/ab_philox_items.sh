@@ -1,6 +1,6 @@
 #!/bin/bash
-# v3 Philox sample items (a full tile's 64 x spp samples handed to whichever lane's path ended) against the same build
-# with items off (every lane renders its own pixel's samples in order; the same Philox windows and fixed-point sums,
+# Philox sample items in v3 and the flat kernel (a full tile's 64 x spp samples handed to whichever lane's path ended)
+# against the same build with items off (every lane renders its own pixel's samples in order; the same Philox windows and fixed-point sums,
 # so the same image).  Same box, bench.py C2 Philox lines, 3 rounds, then C4 Philox and XORWOW C2 as controls.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -20,3 +20,7 @@ for r in 1 2 3; do
 done
 for v in noitems product; do one /tmp/ablib/$v.so "c2 xorwow $v" "--steps 10 --warmup 2"; done
 for v in noitems product; do one /tmp/ablib/$v.so "c4 philox $v" "--config c4 --steps 2 --warmup 1 --rng philox"; done
+for r in 1 2; do
+  for v in noitems product; do one /tmp/ablib/$v.so "c3 philox $v" "--config c3 --steps 2 --warmup 1 --rng philox"; done
+done
+for v in noitems product; do one /tmp/ablib/$v.so "c3 xorwow $v" "--config c3 --steps 2 --warmup 1"; done
