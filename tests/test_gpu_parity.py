@@ -266,6 +266,27 @@ def test_accumulate_first_frame_equals_plain_frame(variant):
     assert np.all(acc2[:, 3] == 2 * cfg.spp) and np.all(acc2[:, :3] >= acc1[:, :3])
 
 
+@pytest.mark.parametrize("variant", [3, 4, 5, 6])
+def test_philox_accumulate_matches_oracle(variant):
+    """Progressive accumulation in Philox mode (the pixel sums in fixed point, sample items on the tile kernels): two
+    frames of the textured case (full 8x8 tiles) accumulate exactly as the oracle's RT_FLAG_ACCUMULATE restatement."""
+    lib().rt_set_variant(variant)
+    case = CASE_BY_NAME["c5_textured_160x96_s4"]
+    cfg = case.cfg()
+    sc = scenes.builtin(cfg.scene)
+    ds = DeviceScene(sc)
+    r = Renderer(cfg.width, cfg.height, rng="philox")
+    r.render_init()
+    acc = np.zeros(cfg.width * cfg.height * 4, dtype=np.float32)
+    for frame in (0, 1):
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=abi.RT_FLAG_ACCUMULATE, frame=frame)
+        torch.cuda.synchronize()
+        ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), None,
+                                philox=True, seed=1984, frame=frame, accum=acc)
+        np.testing.assert_array_equal(r.image(), ref)
+        np.testing.assert_array_equal(r.accum.cpu().numpy().reshape(-1), acc)
+
+
 def test_invalid_arguments_fail_loudly():
     cfg = scenes.CONFIGS["c1"].scaled(32, 16, 1)
     r = Renderer(cfg.width, cfg.height)
