@@ -31,6 +31,7 @@
 #include <mutex>
 #include <tuple>
 #include <type_traits>
+#include <vector>
 
 #include "rt_internal.h"
 #include "rt_scene_device.h"
@@ -2742,9 +2743,10 @@ struct AutoKey {
     void* stream;
     const void* scene;
     uint32_t width, rows, spp, depth, philox;
+    uint32_t flat;  // the trial's pair is the flat kernels (RT_TUNE_FLAT_MAX may change between frames)
     bool operator<(const AutoKey& o) const {
-        return std::tie(device, stream, scene, width, rows, spp, depth, philox) <
-               std::tie(o.device, o.stream, o.scene, o.width, o.rows, o.spp, o.depth, o.philox);
+        return std::tie(device, stream, scene, width, rows, spp, depth, philox, flat) <
+               std::tie(o.device, o.stream, o.scene, o.width, o.rows, o.spp, o.depth, o.philox, o.flat);
     }
 };
 struct AutoChoice {
@@ -2805,12 +2807,16 @@ struct QueueRing {
     size_t slot_bytes = 0;  // (kQueueCounters + 1) heads at the largest stride used so far on the device
     std::atomic<uint32_t> next{0};
     int cus = 0;
+    std::vector<void*> retired;  // rings outgrown by a larger stride: never freed (see acquire_queue)
 };
 QueueRing g_queues[kMaxDevices];
 std::mutex g_queue_mu;
 
 // The next queue slot of `device` for heads `stride` bytes apart.  The ring is sized for the stride in use (2 KB
-// slots at the default 128 B); a larger stride re-allocates it, after the device has drained (hipFree waits).
+// slots at the default 128 B); a larger stride allocates a larger ring.  The outgrown ring is retired, not freed:
+// another thread may hold a head pointer into it, taken under the lock, whose memset and launch it has not yet
+// enqueued (rt_render), so freeing it could hand the kernel freed memory.  Strides are powers of two in
+// [128, kQueueMaxStride], so a device retires at most five rings (≤ 8.9 MB together).
 int acquire_queue(int device, uint32_t stride, uint32_t** head, int* cus) {
     if (device < 0 || device >= kMaxDevices) {
         set_error("rt_render: device ordinal out of range");
@@ -2821,7 +2827,7 @@ int acquire_queue(int device, uint32_t stride, uint32_t** head, int* cus) {
     std::lock_guard<std::mutex> lock(g_queue_mu);
     if (!q.buf || q.slot_bytes < need) {
         if (q.buf) {
-            (void)hipFree(q.buf);
+            q.retired.push_back(q.buf);
             q.buf = nullptr;
         }
         void* p = nullptr;
@@ -3006,6 +3012,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (a->tiling.local_rows == 0 || a->width == 0 || a->height == 0) return RT_OK;  // nothing to render
     const bool philox = (a->flags & RT_FLAG_RNG_PHILOX) != 0;
     if (!a->state && !philox) { set_error("rt_render: state is NULL"); return RT_ERR_INVALID_ARGUMENT; }
+    if (philox && a->samples_per_pixel > RT_PHILOX_MAX_SPP) {  // sample s reads the window at word s << 18
+        set_error("rt_render: RT_FLAG_RNG_PHILOX supports at most RT_PHILOX_MAX_SPP (16384) samples per pixel");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
     if (a->reserved != 0 || a->reserved2 != 0) { set_error("rt_render: reserved fields must be 0"); return RT_ERR_INVALID_ARGUMENT; }
     if (!a->pos && !a->radiance && !a->accum) { set_error("rt_render: no output buffer"); return RT_ERR_INVALID_ARGUMENT; }
     if ((a->flags & RT_FLAG_ACCUMULATE) && !a->accum) { set_error("rt_render: ACCUMULATE without accum"); return RT_ERR_INVALID_ARGUMENT; }
@@ -3135,7 +3145,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
             int device = 0;
             (void)hipGetDevice(&device);
             const AutoKey key{device, stream, scene, a->width, T.local_rows, a->samples_per_pixel, a->max_depth,
-                              philox ? 1u : 0u};
+                              philox ? 1u : 0u, flat_ok ? 1u : 0u};
             std::lock_guard<std::mutex> lock(g_auto_mu);
             auto it = g_auto.find(key);
             if (it == g_auto.end()) {

@@ -222,6 +222,8 @@ uint64_t rt_soa_plane_words(uint32_t width, uint32_t local_rows);
 int rt_render_init_soa(uint32_t* d_planes, uint32_t width, uint32_t height, const rt_tiling* tiling,
                        uint64_t seed_base, rt_stream stream);
 
+#define RT_PHILOX_MAX_SPP 16384u /* RT_FLAG_RNG_PHILOX: samples per pixel (2^14 windows of 2^18 words) */
+
 enum rt_render_flags {
     RT_FLAG_FAITHFUL_GRID = 1u << 0, /* skip pixels outside whole 16×16 blocks (Kernel.cu:184) */
     RT_FLAG_NO_STATE_WRITEBACK = 1u << 1, /* do not store the advanced RNG state (benchmark repeatability) */
@@ -243,7 +245,11 @@ enum rt_render_flags {
                                       the samples run in — the kernels hand a tile's samples to whichever lane
                                       is free.  `state` is neither read nor written (may be NULL): no per-pixel
                                       RNG bytes in HBM.  Not the reference's stream (its images match the parity
-                                      mode statistically, not bit for bit). */
+                                      mode statistically, not bit for bit).  Limits: spp <= RT_PHILOX_MAX_SPP
+                                      (each sample's window is 2^18 words; larger spp is rejected); a sample's
+                                      channel below 2^-13 (and any negative or NaN value) rounds to 0, so a
+                                      very dim image loses up to 2^-13 per sample and channel against the
+                                      parity mode's float sum (tests/test_gpu_parity.py dim-scene check). */
     RT_FLAG_STATE_SOA = 1u << 6    /* `state` holds the XORWOW states as six uint32 planes (rt_render_init_soa)
                                       instead of rt_curand_state structs: the same streams and images, 24 B
                                       per pixel read and written with coalesced 4-B accesses (the 48-B

@@ -65,3 +65,18 @@ def test_soa_plane_words_cover_whole_tiles():
     assert lib().rt_soa_plane_words(7680, 544) == 960 * 68 * 64
     assert lib().rt_soa_plane_words(1, 1) == 64
     assert lib().rt_soa_plane_words(0, 5) == 0
+
+
+def test_philox_spp_limit_is_rejected_before_any_device_work():
+    """RT_FLAG_RNG_PHILOX reads sample s's window at word s << 18 of the pixel's stream (include/rt_hip.h
+    RT_PHILOX_MAX_SPP): above 2^14 samples the oracle's 32-bit word counter would wrap, so rt_render rejects the
+    call — checked here before the scene is touched, so no GPU is needed."""
+    a = abi.RenderArgs()
+    a.width, a.height, a.max_depth = 8, 8, 4
+    a.tiling.band_rows, a.tiling.num_ranks, a.tiling.rank, a.tiling.local_rows = 8, 1, 0, 8
+    a.flags = abi.RT_FLAG_RNG_PHILOX
+    dummy = C.create_string_buffer(64)  # never dereferenced: the limit is checked first
+    for spp in (16385, 1 << 16, 1 << 20):
+        a.samples_per_pixel = spp
+        assert lib().rt_render(C.cast(dummy, C.c_void_p), C.byref(a), None) == -1, spp
+        assert b"RT_PHILOX_MAX_SPP" in lib().rt_last_error()
