@@ -50,9 +50,10 @@ from cudaraytracer_amd import parallel  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ≈ 8 TB/s per GPU
-# SURVEY.md §8(d) D4 counted-flop model: AABB test 21, sphere test 23, shading/sky/sampling 60 per ray,
-# camera ray 40 per primary sample.
-FLOP_BOX, FLOP_PRIM, FLOP_RAY, FLOP_PRIMARY = 21, 23, 60, 40
+# SURVEY.md §8(d) D4 counted-flop model: AABB test 21, sphere test 23, rectangle test 12, shading/sky/sampling
+# 60 per ray, camera ray 40 per primary sample.  The kernel counts sphere and rectangle tests apart
+# (RT_FLAG_COUNT_TESTS: counters[2] all primitive tests, counters[16] the rectangle tests among them).
+FLOP_BOX, FLOP_SPHERE, FLOP_RECT, FLOP_RAY, FLOP_PRIMARY = 21, 23, 12, 60, 40
 F_REF_PER_RAY = 21 * 50.7 + 23 * 6.9 + 60  # reference BVH on C2: ≈1.28 kFLOP/ray
 C5_FRAMES = 60  # C5's scripted orbit (scenes.moving_camera)
 
@@ -64,7 +65,8 @@ METRICS = {
 }
 DATA = {
     "c2": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
-    "c3": "synthetic: Cornell box of 6 rects (5 Lambertian walls + a DiffuseLight), black background",
+    "c3": "synthetic: Cornell box of 6 rects (5 Lambertian walls + a DiffuseLight) and 2 spheres (glass, "
+          "aluminium metal), black background",
     "c4": "synthetic: RTIOW final scene (488 spheres) generated from glibc rand() seed 1",
     "c5": "synthetic: 3 image-textured spheres + ground, three procedural 8192x4096 RGB8 textures "
           "(the reference's asset size; its JPEGs are not decoded here), scripted orbit camera",
@@ -339,7 +341,7 @@ def run_rank(args) -> dict | None:
              flags=frame_flags | abi.RT_FLAG_COUNT_TESTS | abi.RT_FLAG_NO_STATE_WRITEBACK)
     torch.cuda.synchronize()
     c = [int(x) for x in r.counters.tolist()]
-    f_launch = FLOP_BOX * c[1] + FLOP_PRIM * c[2] + FLOP_RAY * c[0] + FLOP_PRIMARY * c[3]
+    f_launch = flop_model(c)
 
     frame_no = [0]
 
@@ -467,6 +469,14 @@ def run_rank(args) -> dict | None:
     return line if rank == 0 else None
 
 
+def flop_model(c) -> int:
+    """SURVEY.md §8(d) D4 FLOP per launch from the counting pass's counters (rays, box tests, primitive tests,
+    primary samples; [16] = the rectangle tests among the primitive tests)."""
+    rects = c[16]
+    spheres = c[2] - rects
+    return FLOP_BOX * c[1] + FLOP_SPHERE * spheres + FLOP_RECT * rects + FLOP_RAY * c[0] + FLOP_PRIMARY * c[3]
+
+
 def valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world) -> dict:
     """VALU-bound roofline: counted algorithmic FLOP of rank 0's launch ÷ the kernel
     time (max over ranks), against the FP32 vector peak; HBM bytes from the committed PMC summary."""
@@ -508,6 +518,10 @@ def valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world) -> dict:
         "flop_per_ray_ref_bvh": round(F_REF_PER_RAY, 1),
         "box_tests_per_ray": round(c[1] / max(1, c[0]), 2),
         "prim_tests_per_ray": round(c[2] / max(1, c[0]), 2),
+        "sphere_tests_per_ray": round((c[2] - c[16]) / max(1, c[0]), 2),
+        "rect_tests_per_ray": round(c[16] / max(1, c[0]), 2),
+        "flop_model": f"{FLOP_BOX}/box + {FLOP_SPHERE}/sphere + {FLOP_RECT}/rect + {FLOP_RAY}/ray + "
+                      f"{FLOP_PRIMARY}/primary (SURVEY D4)",
         "rays_per_launch_rank0": c[0],
     }
 

@@ -21,6 +21,8 @@ RT_FLAG_RIUS_LEFT_TO_RIGHT = 1 << 3
 RT_FLAG_COUNT_TESTS = 1 << 4
 RT_FLAG_RNG_PHILOX = 1 << 5
 RT_FLAG_STATE_SOA = 1 << 6
+COUNTERS_WORDS = 24  # RT_COUNTERS_WORDS: the counters buffer with RT_FLAG_COUNT_TESTS
+PHILOX_MAX_SPP = 16384  # RT_PHILOX_MAX_SPP
 # rt_set_tuning keys (rt_tuning_key in include/rt_hip.h)
 RT_TUNE_REGEN_THRESHOLD, RT_TUNE_LEAF_MAX, RT_TUNE_PERSISTENT_WAVES, RT_TUNE_SAH_TRAVERSAL = 0, 1, 2, 3
 RT_TUNE_LDS_PAD, RT_TUNE_ADAPTIVE_ORDER, RT_TUNE_TEXEL_LAYOUT, RT_TUNE_QUEUE_CHUNK = 4, 5, 6, 7

@@ -277,7 +277,8 @@ struct ScratchStack {
 
 struct Counts {
     uint32_t rays, boxes, prims, primary;
-    uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
+    uint32_t wnode, wleaf, wshade;
+    uint32_t rects = 0;  // COUNT_TESTS: the part of `prims` that are rectangle tests (12 FLOP vs a sphere's 23)  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
     uint32_t wnode_uniform = 0, wleaf_uniform = 0;  // COUNT_TESTS (v3): ... of them with one node / primitive
     uint64_t ctrav = 0, cshade = 0, ctotal = 0, cleaf = 0;  // COUNT_TESTS (v3): wave clock cycles per phase
     // COUNT_TESTS (v3): idle lanes summed over node iterations: pixel done / ray finished, waiting for the
@@ -362,6 +363,7 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
             const uint32_t type = __float_as_uint(p1.w) & 15u;
             if (COUNT) {
                 cnt.prims++;
+                cnt.rects += type != RT_SPHERE ? 1u : 0u;
                 cnt.wleaf += wave_leader();
             }
             if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
@@ -715,6 +717,7 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt
             atomicAdd(&P.counters[13], (unsigned long long)cnt.idle_nt);
             atomicAdd(&P.counters[14], (unsigned long long)cnt.idle_fin);
             atomicAdd(&P.counters[15], (unsigned long long)cnt.idle_wait);
+            atomicAdd(&P.counters[16], (unsigned long long)cnt.rects);
             if (cnt.ctotal && wave_leader()) {  // one lane per wave: the stamps are wave-uniform
                 atomicAdd(&P.counters[7], (unsigned long long)cnt.ctrav);
                 atomicAdd(&P.counters[8], (unsigned long long)cnt.cshade);
@@ -1157,6 +1160,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
                         const uint32_t type = __float_as_uint(p1.w) & 15u;
                         if (COUNT_TESTS) {
                             cnt.prims++;
+                            cnt.rects += type != RT_SPHERE ? 1u : 0u;
                             cnt.wleaf += wave_leader();
                         }
                         if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
@@ -1594,6 +1598,7 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
                 const uint32_t type = __float_as_uint(p1.w) & 15u;
                 if (COUNT_TESTS) {
                     cnt.prims++;
+                    cnt.rects += type != RT_SPHERE ? 1u : 0u;
                     cnt.wleaf += wave_leader();
                     if (__ballot(cur != (uint32_t)__builtin_amdgcn_readfirstlane(cur)) == 0) cnt.wleaf_uniform += wave_leader();
                 }
@@ -2166,7 +2171,10 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
         const ConstF32* q = (const ConstF32*)((const ConstU8*)prims + i * 32u);
         const float4 q0 = make_float4(q[0], q[1], q[2], q[3]), q1 = make_float4(q[4], q[5], q[6], q[7]);
         const uint32_t type = __float_as_uint(q1.w) & 15u;
-        if (COUNT_TESTS) cnt.prims++;
+        if (COUNT_TESTS) {
+            cnt.prims++;
+            cnt.rects += type != RT_SPHERE ? 1u : 0u;
+        }
         if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
             const f3 oc = sub(ro, xyz(q0));
             const float b = dot(oc, rd);

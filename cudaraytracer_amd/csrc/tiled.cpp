@@ -135,7 +135,7 @@ int rt_tiled_create(const rt_tiled_desc* desc, const rt_scene_desc* scene, rt_ti
         if (int rc = hip_err(hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking), "hipStreamCreate")) return rc;
         for (hipEvent_t& e : k.ev)
             if (int rc = hip_err(hipEventCreate(&e), "hipEventCreate")) return rc;
-        if (int rc = hip_err(hipMalloc((void**)&k.counters, 16 * sizeof(uint64_t)), "counter allocation")) return rc;
+        if (int rc = hip_err(hipMalloc((void**)&k.counters, RT_COUNTERS_WORDS * sizeof(uint64_t)), "counter allocation")) return rc;
         if (k.local_rows == 0) continue;
         const size_t px = (size_t)W * k.local_rows;
         if (int rc = hip_err(hipMalloc((void**)&k.pos, px * 4), "framebuffer allocation")) return rc;
@@ -203,7 +203,7 @@ int rt_tiled_render(rt_tiled* t, const rt_tiled_frame* f, rt_tiled_timing* timin
         rt_tiled::Rank& k = t->ranks[r];
         if (int rc = hip_err(hipSetDevice(k.device), "hipSetDevice")) return drain(rc);
         if (int rc = hip_err(hipEventRecord(k.ev[0], k.stream), "hipEventRecord")) return drain(rc);
-        if (int rc = hip_err(hipMemsetAsync(k.counters, 0, 16 * sizeof(uint64_t), k.stream), "counter reset"))
+        if (int rc = hip_err(hipMemsetAsync(k.counters, 0, RT_COUNTERS_WORDS * sizeof(uint64_t), k.stream), "counter reset"))
             return drain(rc);
         if (k.local_rows) {
             rt_render_args a{};

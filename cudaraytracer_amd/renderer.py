@@ -95,7 +95,7 @@ class Renderer:
         self.pos = torch.zeros(n, dtype=torch.int32, device=self.device)
         words = n * abi.STATE_WORDS if state_layout == "curand" else 6 * int(lib().rt_soa_plane_words(width, self.local_rows))
         self.state = torch.zeros(words, dtype=torch.int32, device=self.device) if rng == "xorwow" else None
-        self.counters = torch.zeros(16, dtype=torch.int64, device=self.device)
+        self.counters = torch.zeros(abi.COUNTERS_WORDS, dtype=torch.int64, device=self.device)
         self.radiance = None
         self.accum = None
 

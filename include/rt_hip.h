@@ -222,6 +222,7 @@ uint64_t rt_soa_plane_words(uint32_t width, uint32_t local_rows);
 int rt_render_init_soa(uint32_t* d_planes, uint32_t width, uint32_t height, const rt_tiling* tiling,
                        uint64_t seed_base, rt_stream stream);
 
+#define RT_COUNTERS_WORDS 24u /* rt_render_args.counters length with RT_FLAG_COUNT_TESTS (16 without) */
 #define RT_PHILOX_MAX_SPP 16384u /* RT_FLAG_RNG_PHILOX: samples per pixel (2^14 windows of 2^18 words) */
 
 enum rt_render_flags {
@@ -233,7 +234,8 @@ enum rt_render_flags {
                                              only build of the reference available here; C++ leaves the order
                                              unspecified and nvcc's is not established).
                                              Both orders are tested against the oracle on every config. */
-    RT_FLAG_COUNT_TESTS = 1u << 4, /* also count box and primitive tests into counters[1], [2] */
+    RT_FLAG_COUNT_TESTS = 1u << 4, /* also count box, primitive and rectangle tests into counters[1], [2], [16]
+                                      (counters must then hold RT_COUNTERS_WORDS words) */
     RT_FLAG_RNG_PHILOX = 1u << 5,  /* perf-mode RNG: sample s of a pixel draws from the hipRAND/rocRAND
                                       Philox4x32-10 stream rocrand_init(rng_seed, subsequence = global pixel
                                       index, offset = (rng_frame << 34) + (s << 18)), read as rocrand_uniform4
@@ -262,11 +264,14 @@ typedef struct rt_render_args {
     float* accum;             /* RT_FLAG_ACCUMULATE: device float4 running sum of samples */
     rt_curand_state* state;   /* device RNG states, local_rows × width (RT_FLAG_STATE_SOA: the six planes) */
     uint64_t* counters;       /* optional device uint64[16]: rays, box tests, primitive tests, primary samples;
-                                 with RT_FLAG_COUNT_TESTS also [4..6] = wave-level iterations of node visits,
+                                 with RT_FLAG_COUNT_TESTS it must hold RT_COUNTERS_WORDS (24) words:
+                                 also [4..6] = wave-level iterations of node visits,
                                  primitive tests and shading (SIMD-efficiency diagnostics) and, for the v3
                                  kernels, [7..10] = wave clock cycles spent tracing, shading, in total and
                                  in leaves, [11..12] = node / primitive wave-iterations whose active lanes
-                                 all test the same node / primitive */
+                                 all test the same node / primitive, [13..15] = idle lanes per node iteration
+                                 (pixel done, ray finished, holding a leaf), [16] = rectangle tests (the
+                                 part of [2] that are XY/XZ/YZRect::Hit; the FLOP model prices them apart) */
     uint32_t width;
     uint32_t height;          /* global image height */
     uint32_t samples_per_pixel;

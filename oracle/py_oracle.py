@@ -21,7 +21,7 @@ _lib = None
 
 class Counters(C.Structure):
     _fields_ = [("rays", C.c_ulonglong), ("box_tests", C.c_ulonglong), ("prim_tests", C.c_ulonglong),
-                ("primary", C.c_ulonglong)]
+                ("primary", C.c_ulonglong), ("rect_tests", C.c_ulonglong)]
 
 
 class Hit(C.Structure):

@@ -507,13 +507,14 @@ int orc_scene_depth(const orc_scene* s) { return s->depth; }
 typedef struct { int node; float tmin, tmax; } stacknode;
 
 static int world_hit(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, hitrec* rec,
-                     unsigned long long* box_tests, unsigned long long* prim_tests) {
+                     unsigned long long* box_tests, unsigned long long* prim_tests, unsigned long long* rect_tests) {
     if (s->exact_closest_hit) {
         /* Geometric closest hit over the active primitives in list order, without box culling. */
         int hit_something = 0;
         for (int i = 0; i < s->nprims; i++) {
             if (!s->prims[i].is_active) continue;
             ++*prim_tests;
+            *rect_tests += s->prims[i].type != RT_SPHERE;
             hit_something |= prim_hit(&s->prims[i], o, d, tmin, hit_something ? rec->t : tmax, rec);
         }
         return hit_something;
@@ -536,6 +537,7 @@ static int world_hit(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, hit
                 stack[++top] = (stacknode){ch[k].idx, cur.tmin, hit_something ? rec->t : cur.tmax};
             } else if (ch[k].kind == 2) {
                 ++*prim_tests;
+                *rect_tests += s->prims[ch[k].idx].type != RT_SPHERE;
                 hit_something |= prim_hit(&s->prims[ch[k].idx], o, d, cur.tmin, hit_something ? rec->t : cur.tmax, rec);
             }
         }
@@ -642,7 +644,7 @@ static v3 color(const orc_scene* s, v3 o, v3 d, int max_depth, orc_rng* st, cons
     memset(&rec, 0, sizeof(rec));
     for (int i = 0; i < max_depth; i++) {
         c->rays++;
-        if (!world_hit(s, o, d, 0.001f, FLT_MAX, &rec, &c->box_tests, &c->prim_tests)) {
+        if (!world_hit(s, o, d, 0.001f, FLT_MAX, &rec, &c->box_tests, &c->prim_tests, &c->rect_tests)) {
             v3 unit_direction = unit_vector(d);
             float t = 0.5f * (unit_direction.y + 1.0f);
             v3 bg = add(scale(1.0f - t, ld3(in->background_start)), scale(t, ld3(in->background_end)));
@@ -706,14 +708,14 @@ void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, float* a
     v3 origin = ld3(in->origin), fwd = ld3(in->orientation), up = ld3(in->up);
     v3 right = normalize(cross(up, fwd));
     v3 center = mk(width / 2.0f, height / 2.0f, 0.0f);
-    unsigned long long rays = 0, boxes = 0, prims = 0, primary = 0;
+    unsigned long long rays = 0, boxes = 0, prims = 0, primary = 0, rects = 0;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : rays, boxes, prims, primary)
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : rays, boxes, prims, primary, rects)
 #endif
     for (long ri = 0; ri < nrows; ri++) {
         int y = (int)(row_begin + (unsigned)ri * row_step);
-        orc_counters c = {0, 0, 0, 0};
+        orc_counters c = {0, 0, 0, 0, 0};
         for (int x = 0; x < (int)gw; x++) {
             unsigned pixel_index = (unsigned)y * width + (unsigned)x;
             rt_curand_state st;
@@ -769,10 +771,11 @@ void orc_render(const orc_scene* s, unsigned int* pos, float* radiance, float* a
             col.z = 255.0f * sqrtf(col.z);
             pos[pixel_index] = orc_rgb_to_int(col.x, col.y, col.z);
         }
-        rays += c.rays; boxes += c.box_tests; prims += c.prim_tests; primary += c.primary;
+        rays += c.rays; boxes += c.box_tests; prims += c.prim_tests; primary += c.primary; rects += c.rect_tests;
     }
     if (counters) {
         counters->rays = rays; counters->box_tests = boxes; counters->prim_tests = prims; counters->primary = primary;
+        counters->rect_tests = rects;
     }
 }
 

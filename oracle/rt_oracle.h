@@ -53,9 +53,11 @@ float orc_atan2(float y, float x);
 void orc_render_init(rt_curand_state* state, unsigned width, unsigned height, unsigned long long seed_base,
                      int full);
 
-/* Counters: [0] rays (color() iterations, Kernel.cu:39), [1] AABB tests, [2] primitive tests, [3] primary */
+/* Counters: [0] rays (color() iterations, Kernel.cu:39), [1] AABB tests, [2] primitive tests, [3] primary,
+ * [4] rectangle tests (the part of [2] that are XY/XZ/YZRect::Hit, Hittable.cuh:140-281; SURVEY §8(d) D4 prices
+ * them at 12 FLOP against a sphere test's 23) */
 typedef struct orc_counters {
-    unsigned long long rays, box_tests, prim_tests, primary;
+    unsigned long long rays, box_tests, prim_tests, primary, rect_tests;
 } orc_counters;
 
 /* One frame of Kernel (Kernel.cu:102-158).  pos: W·H uint32 (row 0 = bottom); radiance: optional W·H·4

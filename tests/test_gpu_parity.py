@@ -87,6 +87,22 @@ def test_count_tests_flag_does_not_change_the_image():
     np.testing.assert_array_equal(r.image(), g["pos"])
     rays, boxes, prims = (int(x) for x in r.counters[:3])
     assert boxes > 2 * rays and prims > 0
+    assert int(r.counters[16]) == 0  # RTIOW: spheres only
+
+
+@pytest.mark.parametrize("variant", [3, 5, 6])
+def test_rectangle_tests_are_counted_apart(variant):
+    """counters[16] (RT_FLAG_COUNT_TESTS) is the rectangle part of the primitive tests (bench.py's FLOP model
+    prices them at 12 against a sphere's 23).  The flat kernels (5, 6) test every primitive of
+    C3's Cornell box per ray: 6 rectangles and 2 spheres each; the BVH kernel (3) a subset."""
+    case = CASE_BY_NAME["c3_cornell_128_s16"]
+    r, _, _ = _render(case, variant, count_tests=True)
+    np.testing.assert_array_equal(r.image(), load_golden(case.name)["pos"])
+    rays, prims, rects = int(r.counters[0]), int(r.counters[2]), int(r.counters[16])
+    if variant in (5, 6):
+        assert (prims, rects) == (8 * rays, 6 * rays)
+    else:
+        assert 0 < rects < prims
 
 
 @pytest.mark.parametrize("num_ranks, band_rows", [(2, 16), (3, 16), (4, 8), (8, 16)])

@@ -11,7 +11,7 @@ import struct
 import numpy as np
 import pytest
 
-from cases import CASES, PHILOX_CASES
+from cases import CASE_BY_NAME, CASES, PHILOX_CASES
 from cudaraytracer_amd import abi, scenes
 from helpers import GOLDEN, digest, load_golden
 from oracle import py_oracle as po
@@ -398,3 +398,33 @@ def test_native_cpu_baseline_build_computes_the_checker_bits(tmp_path):
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(st_a, st_b)
     assert ca.rays == cb.rays
+
+
+def test_flop_model_prices_rectangle_and_sphere_tests_apart():
+    """SURVEY §8(d) D4 prices a rectangle test at 12 FLOP and a sphere test at 23.  The oracle counts the rectangle
+    tests among its primitive tests (orc_counters.rect_tests); on the C3 golden (Cornell box: 6 rectangles and 2
+    spheres, builtin_scenes.cpp cornell) the exact closest-hit scan — what the flat kernels execute — tests every
+    primitive per ray, so the split is exactly 6 : 2 per ray, and bench.py's model applies 12 and 23 to it."""
+    import bench
+
+    case = CASE_BY_NAME["c3_cornell_128_s16"]
+    cfg = case.cfg()
+    sc = scenes.builtin(cfg.scene)
+    kinds = [int(h.type) for h in sc.hittables]
+    n_rect = sum(1 for k in kinds if k != abi.RT_SPHERE)
+    assert (n_rect, len(kinds) - n_rect) == (6, 2)
+    inp = cfg.inputs()
+    st = po.init_states(cfg.width, cfg.height)
+    _, _, cnt = po.render(po.OracleScene(sc, exact=True), cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st)
+    assert cnt.prim_tests == 8 * cnt.rays and cnt.rect_tests == 6 * cnt.rays
+    c = [cnt.rays, cnt.box_tests, cnt.prim_tests, cnt.primary] + [0] * 12 + [cnt.rect_tests] + [0] * 7
+    assert len(c) == abi.COUNTERS_WORDS
+    want = 21 * cnt.box_tests + 23 * 2 * cnt.rays + 12 * 6 * cnt.rays + 60 * cnt.rays + 40 * cnt.primary
+    assert bench.flop_model(c) == want
+    # 60 + 2·23 + 6·12 = 178 FLOP per ray plus the camera rays' share (every prim tested at 23 would be 244)
+    assert bench.flop_model(c) / cnt.rays == pytest.approx(178 + 40 * cnt.primary / cnt.rays)
+    # the reference BVH (golden counters) tests a subset; its rectangle tests are a part of its primitive tests
+    st = po.init_states(cfg.width, cfg.height)
+    _, _, ref = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st)
+    assert [ref.rays, ref.box_tests, ref.prim_tests, ref.primary] == [int(x) for x in load_golden(case.name)["counters"]]
+    assert 0 < ref.rect_tests < ref.prim_tests
