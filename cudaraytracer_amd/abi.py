@@ -21,6 +21,7 @@ RT_FLAG_RIUS_LEFT_TO_RIGHT = 1 << 3
 RT_FLAG_COUNT_TESTS = 1 << 4
 RT_FLAG_RNG_PHILOX = 1 << 5
 RT_FLAG_STATE_SOA = 1 << 6
+RT_FLAG_ACCUMULATE_RESET = 1 << 7
 COUNTERS_WORDS = 24  # RT_COUNTERS_WORDS: the counters buffer with RT_FLAG_COUNT_TESTS
 PHILOX_MAX_SPP = 16384  # RT_PHILOX_MAX_SPP
 # rt_set_tuning keys (rt_tuning_key in include/rt_hip.h)

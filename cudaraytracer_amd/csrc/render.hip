@@ -687,7 +687,10 @@ __device__ __forceinline__ void write_pixel(const KParams& P, size_t pix, uint32
     col = pixel_sum(rng, col);
     f3 c;
     if (P.flags & RT_FLAG_ACCUMULATE) {
-        float4 a = acc_pre ? *acc_pre : P.accum[pix];  // (acc_pre: the value loaded when the pixel started)
+        // (acc_pre: the value loaded when the pixel started; RT_FLAG_ACCUMULATE_RESET: a restart, nothing is read and
+        // the sums below are 0 + x, as after a zero fill)
+        float4 a = (P.flags & RT_FLAG_ACCUMULATE_RESET) ? make_float4(0.0f, 0.0f, 0.0f, 0.0f)
+                                                        : (acc_pre ? *acc_pre : P.accum[pix]);
         a.x = a.x + col.x;
         a.y = a.y + col.y;
         a.z = a.z + col.z;
@@ -2453,7 +2456,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
                 g = sg;
                 pix = spix;
                 rng = srng;
-                if (kAcc && accumulate) acc = P.accum[spix];
+                if (kAcc && accumulate && !(P.flags & RT_FLAG_ACCUMULATE_RESET)) acc = P.accum[spix];
                 col = mk(0.0f, 0.0f, 0.0f);
                 sample = 0u;
                 cam = true;
@@ -3027,6 +3030,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (a->reserved != 0 || a->reserved2 != 0) { set_error("rt_render: reserved fields must be 0"); return RT_ERR_INVALID_ARGUMENT; }
     if (!a->pos && !a->radiance && !a->accum) { set_error("rt_render: no output buffer"); return RT_ERR_INVALID_ARGUMENT; }
     if ((a->flags & RT_FLAG_ACCUMULATE) && !a->accum) { set_error("rt_render: ACCUMULATE without accum"); return RT_ERR_INVALID_ARGUMENT; }
+    if ((a->flags & RT_FLAG_ACCUMULATE_RESET) && !(a->flags & RT_FLAG_ACCUMULATE)) {
+        set_error("rt_render: ACCUMULATE_RESET without ACCUMULATE");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
     if (a->width == 0 || a->height == 0) return RT_OK;
     const rt_tiling& T = a->tiling;
     if (T.band_rows == 0 || T.num_ranks == 0 || T.rank >= T.num_ranks) {

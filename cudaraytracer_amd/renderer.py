@@ -98,6 +98,7 @@ class Renderer:
         self.counters = torch.zeros(abi.COUNTERS_WORDS, dtype=torch.int64, device=self.device)
         self.radiance = None
         self.accum = None
+        self._accum_restart = False  # the next accumulating frame restarts the sums (RT_FLAG_ACCUMULATE_RESET)
 
     def tiling(self) -> abi.Tiling:
         return abi.Tiling(self.band_rows, self.num_ranks, self.rank, self.local_rows)
@@ -122,8 +123,13 @@ class Renderer:
         mode draws frame `frame` (default: the next frame counter value) of every pixel's stream."""
         if radiance and self.radiance is None:
             self.radiance = torch.zeros(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
-        if flags & abi.RT_FLAG_ACCUMULATE and self.accum is None:
-            self.accum = torch.zeros(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
+        if flags & abi.RT_FLAG_ACCUMULATE:
+            if self.accum is None:  # (never read before the first frame writes it)
+                self.accum = torch.empty(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
+                self._accum_restart = True
+            if self._accum_restart:
+                flags |= abi.RT_FLAG_ACCUMULATE_RESET
+                self._accum_restart = False
         a = abi.RenderArgs()
         a.pos = self.pos.data_ptr()
         a.radiance = self.radiance.data_ptr() if radiance else None
@@ -148,8 +154,9 @@ class Renderer:
         return self.pos
 
     def reset_accumulation(self) -> None:
-        if self.accum is not None:
-            self.accum.zero_()
+        """Restart the progressive sums (camera move, scene edit): the next accumulating frame passes
+        RT_FLAG_ACCUMULATE_RESET, which writes the accumulator without reading it — no fill kernel."""
+        self._accum_restart = True
 
     def image(self) -> np.ndarray:
         """Local framebuffer as (local_rows, W) uint32 RGBA8 (row 0 = bottom of the image)."""

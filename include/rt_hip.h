@@ -252,6 +252,10 @@ enum rt_render_flags {
                                       channel below 2^-13 (and any negative or NaN value) rounds to 0, so a
                                       very dim image loses up to 2^-13 per sample and channel against the
                                       parity mode's float sum (tests/test_gpu_parity.py dim-scene check). */
+    RT_FLAG_ACCUMULATE_RESET = 1u << 7, /* with RT_FLAG_ACCUMULATE: the accumulation restarts with this frame
+                                            (a camera move or scene edit): accum is written, never read — the
+                                            same bits as zeroing it first (0 + x rounds as the kernel adds),
+                                            without the fill kernel and the read of zeros */
     RT_FLAG_STATE_SOA = 1u << 6    /* `state` holds the XORWOW states as six uint32 planes (rt_render_init_soa)
                                       instead of rt_curand_state structs: the same streams and images, 24 B
                                       per pixel read and written with coalesced 4-B accesses (the 48-B

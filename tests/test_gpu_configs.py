@@ -15,7 +15,7 @@ import pytest
 import torch
 
 from cudaraytracer_amd import abi, scenes
-from cudaraytracer_amd._lib import lib
+from cudaraytracer_amd._lib import RTError, lib
 from cudaraytracer_amd.renderer import DeviceScene, Renderer
 from oracle import py_oracle as po
 
@@ -134,6 +134,44 @@ def test_c5_progressive_moving_camera_bit_exact(rng, order, c5_scene):
         np.testing.assert_array_equal(r.accum.cpu().numpy(), acc, err_msg=f"frame {frame}")
     if st is not None:
         np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
+
+
+@pytest.mark.parametrize("variant", [3, 4, 5, 6])
+@pytest.mark.parametrize("rng", ["xorwow", "philox"])
+def test_accumulate_reset_never_reads_the_accumulator(rng, variant, c5_scene):
+    """RT_FLAG_ACCUMULATE_RESET (a camera move): the frame writes the float4 sums as if the accumulator had been
+    zeroed — bit for bit, whatever it held (NaN here) — so the per-frame fill kernel goes away."""
+    cfg = scenes.CONFIGS["c5"].scaled(96, 64)
+    ds = DeviceScene(c5_scene)
+    inp = list(_c5_schedule(2))[1][0]
+    out = {}
+    lib().rt_set_variant(variant)
+    try:
+        for how in ("zeroed", "reset"):
+            r = Renderer(cfg.width, cfg.height, rng=rng)
+            r.render_init()
+            r.accum = torch.full((cfg.width * cfg.height * 4,), float("nan") if how == "reset" else 0.0,
+                                 dtype=torch.float32, device=r.device)
+            r._accum_restart = False
+            flags = abi.RT_FLAG_ACCUMULATE | (abi.RT_FLAG_ACCUMULATE_RESET if how == "reset" else 0)
+            for frame in range(2):  # the second frame adds to the first
+                r.render(ds, cfg.spp, cfg.depth, inp, flags=flags if frame == 0 else abi.RT_FLAG_ACCUMULATE,
+                         frame=frame if rng == "philox" else None)
+            torch.cuda.synchronize()
+            out[how] = (r.image(), r.accum.cpu().numpy().view(np.uint32))
+    finally:
+        lib().rt_set_variant(-1)
+    np.testing.assert_array_equal(out["reset"][0], out["zeroed"][0])
+    np.testing.assert_array_equal(out["reset"][1], out["zeroed"][1])
+    assert int(np.count_nonzero(out["reset"][0])) > 0
+
+
+def test_accumulate_reset_requires_accumulate():
+    cfg = scenes.CONFIGS["c1"].scaled(16, 16, 1)
+    r = Renderer(cfg.width, cfg.height)
+    r.render_init()
+    with pytest.raises(RTError):
+        r.render(DeviceScene(scenes.builtin(cfg.scene)), 1, 2, cfg.inputs(), flags=abi.RT_FLAG_ACCUMULATE_RESET)
 
 
 @pytest.mark.parametrize("order", list(ORDERS))
