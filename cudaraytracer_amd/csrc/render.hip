@@ -239,8 +239,8 @@ struct KParams {
     uint32_t work_per_counter; // v4: indices per queue head (a multiple of 64): head k owns [k·n, (k+1)·n)
     uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
     uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
-    unsigned long long* wave_trace;  // diagnostic: v3 per tile {start, end}; v4 per wave {start, queue drained,
-                                     // end, pixels} of s_memrealtime (100 MHz)
+    unsigned long long* wave_trace;  // diagnostic: v3 / flat per tile {start, end} of s_memrealtime (100 MHz); the
+                                     // persistent kernels per wave kWaveTraceWords words (trace_persistent_wave)
     unsigned long long wave_trace_words;  // its size; a stamp that would not fit is not written
     const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
@@ -1868,6 +1868,9 @@ struct PixelQueue {
     uint32_t wave_pixels = 0u;             // pixels this wave has taken
     bool drained = false;                  // the frame's queue is empty
     uint64_t rt_drained = 0u;              // (wave trace) when it found the queue empty
+    uint64_t rt_last = 0u;                 // (wave trace) when it last handed a pixel to a lane
+    uint64_t rt_atomic = 0u;               // (wave trace) realtime ticks spent waiting for queue atomics
+    uint32_t n_grab = 0u, n_probe = 0u;    // (wave trace) chunk atomics that returned work / found a head exhausted
     __device__ explicit PixelQueue(uint32_t head) : qc(head) {}
     // Lanes with `need` take the next work indices of the wave's chunk (ballot + mbcnt rank); start(x, g, pix) runs on
     // every lane that gets a pixel, and its `need` clears.  A lane still needing one afterwards found the queue empty.
@@ -1879,15 +1882,26 @@ struct PixelQueue {
                 const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
                 uint32_t base = 0u;
                 const uint32_t want = head_left > 4u * P.work_chunk ? P.work_chunk : 64u;
+                const uint64_t ta = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
                 if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, want);
                 base = __builtin_amdgcn_readlane(base, leader);
                 const uint32_t idx = qc * P.work_per_counter + base;
+                if (P.wave_trace) {  // (diagnostic: the atomic's round trip, stamped after its result is in)
+                    __builtin_amdgcn_s_waitcnt(0);
+                    rt_atomic += __builtin_amdgcn_s_memrealtime() - ta;
+                }
                 if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
                     // mark it in the exhausted-heads word and move to the next live head (so a wave probes a few
                     // heads at the frame's end, not every one of them)
+                    const uint64_t tb = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
                     uint32_t done = 0u;
                     if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * P.queue_stride, 1u << qc);
                     done = __builtin_amdgcn_readlane(done, leader) | (1u << qc);
+                    if (P.wave_trace) {
+                        __builtin_amdgcn_s_waitcnt(0);
+                        rt_atomic += __builtin_amdgcn_s_memrealtime() - tb;
+                        n_probe++;
+                    }
                     if (done == kQueueAllDone || ++qtried >= kQueueCounters) {
                         drained = true;
                         if (P.wave_trace) rt_drained = __builtin_amdgcn_s_memrealtime();
@@ -1900,6 +1914,7 @@ struct PixelQueue {
                     continue;
                 }
                 wq_next = idx;
+                if (P.wave_trace) n_grab++;
                 // (a chunk ends at its head's range: a head's range is a multiple of 64, not of work_chunk)
                 wq_end = idx + min(want, P.work_per_counter - base);
                 head_left = P.work_per_counter - base - min(want, P.work_per_counter - base);
@@ -1916,12 +1931,33 @@ struct PixelQueue {
             }
             const uint32_t taken = min((uint32_t)__popcll(needm), avail);
             wq_next += taken;
+            if (P.wave_trace && taken) rt_last = __builtin_amdgcn_s_memrealtime();
             const uint64_t still = __ballot(need);
             wave_pixels += (uint32_t)__popcll(needm & ~still);
             needm = still;
         }
     }
 };
+
+// Wave trace of the persistent kernels (rt_set_wave_trace; tools/v4_timeline.py), kWaveTraceWords words per wave:
+// [0] start, [1] queue found empty, [2] end, [3] pixels taken, [4] HW_REG_HW_ID | HW_REG_XCC_ID << 32 (the wave's
+// SIMD / CU / shader engine and XCD), [5] when it last handed out a pixel, [6] chunk grabs | exhausted-head probes
+// << 32, [7] realtime ticks spent waiting for the queue's atomics.  Times: s_memrealtime (100 MHz).
+constexpr uint32_t kWaveTraceWords = 8;
+__device__ __forceinline__ void trace_persistent_wave(const KParams& P, const PixelQueue& queue, uint64_t rt_start) {
+    if (P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (blockIdx.x + 1ull) <= P.wave_trace_words) {
+        unsigned long long* w = P.wave_trace + (size_t)kWaveTraceWords * blockIdx.x;
+        w[0] = rt_start;
+        w[1] = queue.rt_drained;
+        w[2] = __builtin_amdgcn_s_memrealtime();
+        w[3] = queue.wave_pixels;
+        w[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+               ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
+        w[5] = queue.rt_last;
+        w[6] = (unsigned long long)queue.n_grab | ((unsigned long long)queue.n_probe << 32);
+        w[7] = queue.rt_atomic;
+    }
+}
 
 template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false, int WAVES_PER_SIMD = 1>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
@@ -2006,13 +2042,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     cnt.rays = park[PK_RAYS * 64];
     // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
     cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;
-    if (P.wave_trace && wave_leader() && 4ull * blockIdx.x + 4ull <= P.wave_trace_words) {  // (tools/v4_timeline.py)
-        unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
-        w[0] = rt_start;
-        w[1] = queue.rt_drained;
-        w[2] = __builtin_amdgcn_s_memrealtime();
-        w[3] = queue.wave_pixels;
-    }
+    trace_persistent_wave(P, queue, rt_start);
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
@@ -2495,13 +2525,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     }
     cnt.rays = rays;
     cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
-    if (P.wave_trace && wave_leader() && 4ull * blockIdx.x + 4ull <= P.wave_trace_words) {  // (tools/v4_timeline.py)
-        unsigned long long* w = P.wave_trace + 4u * blockIdx.x;
-        w[0] = rt_start;
-        w[1] = queue.rt_drained;
-        w[2] = __builtin_amdgcn_s_memrealtime();
-        w[3] = queue.wave_pixels;
-    }
+    trace_persistent_wave(P, queue, rt_start);
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 

@@ -453,3 +453,35 @@ def test_whole_frame_bit_exact(config, spp, variant):
     assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
     np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
     assert int(r.counters[0]) == cnt.rays
+
+
+@pytest.mark.parametrize("variant", [4, 6])
+def test_persistent_wave_trace_accounts_for_every_pixel(variant, c5_scene):
+    """The persistent kernels' 8-word wave trace (rt_set_wave_trace, tools/c5_tail.py): the waves' pixel counts add
+    up to the frame, stamps are ordered, the XCD ids are those of the device's 8 XCDs, and tracing does not change
+    the image."""
+    cfg = scenes.CONFIGS["c5"].scaled(256, 128)
+    ds = DeviceScene(c5_scene)
+    lib().rt_set_variant(variant)
+    trace = torch.zeros(8 * 8192, dtype=torch.int64, device="cuda")
+    imgs = []
+    try:
+        for traced in (False, True):
+            r = Renderer(cfg.width, cfg.height)
+            r.render_init()
+            lib().rt_set_wave_trace(trace.data_ptr() if traced else None, trace.numel())
+            r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+            torch.cuda.synchronize()
+            lib().rt_set_wave_trace(None, 0)
+            imgs.append(r.image())
+    finally:
+        lib().rt_set_variant(-1)
+    np.testing.assert_array_equal(imgs[0], imgs[1])
+    t = trace.cpu().numpy().view(np.uint64).reshape(-1, 8)
+    t = t[t[:, 0] > 0]
+    assert int(t[:, 3].sum()) == cfg.width * cfg.height
+    assert np.all(t[:, 2] >= t[:, 0])
+    xcc = (t[:, 4] >> 32) & 0xF
+    assert set(np.unique(xcc).tolist()) <= set(range(8))
+    grabs = t[:, 6] & 0xFFFFFFFF
+    assert int(grabs.sum()) >= (cfg.width * cfg.height) // 64

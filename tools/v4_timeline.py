@@ -32,7 +32,7 @@ args = ap.parse_args()
 c5 = scenes.CONFIGS["c5"]
 ds5 = DeviceScene(c5.scene_desc())
 ds2 = DeviceScene(scenes.builtin(scenes.CONFIGS["c2"].scene))
-trace = torch.zeros(4 * 65536, dtype=torch.int64, device="cuda")
+trace = torch.zeros(8 * 65536, dtype=torch.int64, device="cuda")  # 8 words per wave (kWaveTraceWords)
 
 
 def run(ds, cfg, spp, depth, flags, rng="xorwow", layout="soa", n=None, traced=True):
@@ -53,7 +53,7 @@ def run(ds, cfg, spp, depth, flags, rng="xorwow", layout="soa", n=None, traced=T
         torch.cuda.synchronize()
         lib().rt_set_wave_trace(None, 0)
         times.append(lib().rt_last_kernel_ms())
-        t = trace.cpu().numpy().reshape(-1, 4)
+        t = trace.cpu().numpy().reshape(-1, 8)
         t = t[t[:, 0] > 0].astype(np.float64)
         if traced and len(t):
             spans.append(t)
