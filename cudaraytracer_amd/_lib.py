@@ -41,6 +41,9 @@ EXPORTED = [
     "rt_set_timing",
     "rt_set_wave_trace",
     "rt_set_tile_order",
+    "rt_set_pixel_cost",
+    "rt_set_ray_dump",
+    "rt_trace_rays",
     "rt_last_kernel_ms",
     "rt_last_variant",
     "rt_last_launch_host_ms",
@@ -89,6 +92,9 @@ def _declare(lib: C.CDLL) -> None:
     lib.rt_write_ppm.argtypes = [C.c_char_p, vp, C.c_uint32, C.c_uint32, C.c_int]
     lib.rt_set_wave_trace.argtypes = [C.c_void_p, C.c_uint64]
     lib.rt_set_tile_order.argtypes = [C.c_void_p]
+    lib.rt_set_pixel_cost.argtypes = [C.c_void_p, C.c_uint64]
+    lib.rt_set_ray_dump.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+    lib.rt_trace_rays.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     lib.rt_last_kernel_ms.restype = C.c_float
     lib.rt_last_variant.restype = C.c_int
     lib.rt_last_launch_host_ms.restype = C.c_float

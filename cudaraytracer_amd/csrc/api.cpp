@@ -109,6 +109,7 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.num_nodes = h.num_nodes;
     d.num_prims = h.num_prims;
     d.num_mats = h.num_mats;
+    d.num_imgs = (uint32_t)(h.imgs.size() / 4);
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;

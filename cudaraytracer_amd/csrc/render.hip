@@ -217,6 +217,7 @@ struct KParams {
     uint32_t state_stride;  // distance between a pixel's state words: 1 (rt_curand_state) or the plane size
     unsigned long long* counters;
     uint32_t num_nodes, num_prims;
+    uint32_t num_mats, num_imgs;  // material / image table entries (the persistent flat kernel stages them in LDS)
     uint32_t width, height, spp, max_depth, flags;
     uint32_t band_rows, num_ranks, rank, local_rows;
     uint32_t tiles_x;
@@ -242,7 +243,12 @@ struct KParams {
     unsigned long long* wave_trace;  // diagnostic: v3 / flat per tile {start, end} of s_memrealtime (100 MHz); the
                                      // persistent kernels per wave kWaveTraceWords words (trace_persistent_wave)
     unsigned long long wave_trace_words;  // its size; a stamp that would not fit is not written
-    const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major)
+    const uint32_t* tile_order;      // v3: launch order of the 8×8 tiles (NULL = row-major); persistent kernels: the
+                                     // tile of work tile slot i (the queue hands out slots in order)
+    uint8_t* pixel_cost;             // persistent flat: per work index, the passes its pixel took (cost-ordered queue)
+    float4* ray_dump;                // diagnostic (v3, COUNT_TESTS builds): rays that start at bounce ray_dump_depth,
+    uint32_t* ray_dump_count;        // appended as (origin, 0), (direction, 0) pairs; the count of rays offered
+    uint32_t ray_dump_cap, ray_dump_depth;  // (rt_set_ray_dump; tools/coherence.py)
     uint32_t* tile_cost;             // v3: per tile, the wave's lifetime (s_memtime cycles / 256) of this launch
     uint32_t num_tiles;              // v3: tiles of the (local) image; slots beyond it carry no tile
     uint32_t regen_live_frac;        // v3: threshold cap as a fraction of the wave's live pixels (x/64; 0 = off)
@@ -277,8 +283,8 @@ struct ScratchStack {
 
 struct Counts {
     uint32_t rays, boxes, prims, primary;
-    uint32_t wnode, wleaf, wshade;
-    uint32_t rects = 0;  // COUNT_TESTS: the part of `prims` that are rectangle tests (12 FLOP vs a sphere's 23)  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
+    uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
+    uint32_t rects = 0;  // COUNT_TESTS: the part of `prims` that are rectangle tests (12 FLOP vs a sphere's 23)
     uint32_t wnode_uniform = 0, wleaf_uniform = 0;  // COUNT_TESTS (v3): ... of them with one node / primitive
     uint64_t ctrav = 0, cshade = 0, ctotal = 0, cleaf = 0;  // COUNT_TESTS (v3): wave clock cycles per phase
     // COUNT_TESTS (v3): idle lanes summed over node iterations: pixel done / ray finished, waiting for the
@@ -526,14 +532,15 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 // and att are untouched, and the lane shades the same hit again at the next pass, continuing the same call.
 enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1, SHADE_DEFERRED = 2 };
 template <bool TEX = true, bool DEFER = false, class PP, class R>
-__device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int hit, uint32_t hit_tag, float t,
+__device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, const float4* __restrict__ mats,
+                                     const int4* __restrict__ imgs, int hit, uint32_t hit_tag, float t,
                                      f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
     // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
     // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
     // primitive — the material load need not wait for the primitive's
     uint32_t mtype = 0xffu;  // 0xff: miss
-    if (hit >= 0) mtype = __float_as_uint(P->mats[3 * (hit_tag >> 4)].x) & 15u;
+    if (hit >= 0) mtype = __float_as_uint(mats[3 * (hit_tag >> 4)].x) & 15u;
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
     if (hit < 0) {  // sky (Kernel.cu:41-44)
         // rd.y / |rd|: below |rd.y| = 2^-100 the quotient's exact bits vanish in the + 1 (|q| < 2^-60)
@@ -549,7 +556,7 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
     const float4 p0 = prims[2 * hit + 0];
     const float4 p1 = prims[2 * hit + 1];
     const uint32_t type = hit_tag & 15u, mat = hit_tag >> 4;
-    const float4 m0 = P->mats[3 * mat + 0];
+    const float4 m0 = mats[3 * mat + 0];
     const uint32_t ttype = (__float_as_uint(m0.x) >> 4) & 15u;
     f3 p, normal;
     float hu = 0.0f, hv = 0.0f;
@@ -577,11 +584,11 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         p = add(ro, scale(t, rd));
     }
     if (mtype == RT_DIFFUSELIGHT) {  // DiffuseLight::Emitted (Material.cuh:164-176)
-        const float4 m1 = P->mats[3 * mat + 1];
+        const float4 m1 = mats[3 * mat + 1];
         f3 tex = xyz(m1);
         if (TEX && ttype != RT_CONSTANT) {
-            const float4 m2 = P->mats[3 * mat + 2];
-            tex = texture_value(m0, m1, m2, ttype, hu, hv, p, P->imgs, P->texels);
+            const float4 m2 = mats[3 * mat + 2];
+            tex = texture_value(m0, m1, m2, ttype, hu, hv, p, imgs, P->texels);
         }
         const f3 e = scale(m0.z, tex);
         contrib = mulv(e, att);
@@ -599,7 +606,7 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
         // reference computes (pure functions of rd, normal, ir), and only the chosen direction is formed.
         // m1 = (1.0f / ir, r0²) precomputed on the host with the same operations (rt_internal.h).
         const float ir = m0.y;
-        const float4 m1 = P->mats[3 * mat + 1];
+        const float4 m1 = mats[3 * mat + 1];
         const float dn = dot(rd, normal);
         const bool exiting = dn > 0.0f;
         const float cn = exiting ? dn : -dn;
@@ -636,7 +643,7 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
     } else {
         q = random_in_unit_sphere(rng, rtl);
     }
-    const float4 m1 = P->mats[3 * mat + 1];
+    const float4 m1 = mats[3 * mat + 1];
     f3 attenuation;
     bool ok = true;
     if (mtype == RT_LAMBERTIAN) {  // Lambertian::Scatter (Material.cuh:43-62)
@@ -650,8 +657,8 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, int
     if (!TEX || ttype == RT_CONSTANT) {
         attenuation = xyz(m1);
     } else {
-        const float4 m2 = P->mats[3 * mat + 2];
-        attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, P->imgs, P->texels);
+        const float4 m2 = mats[3 * mat + 2];
+        attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, imgs, P->texels);
     }
     ro = p;
     if (ok) {
@@ -1014,7 +1021,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
                 float t;
                 const int hit = trace<COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, cnt);
                 if (COUNT_TESTS) cnt.wshade += wave_leader();
-                done = shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+                done = shade(&P, prims, P.mats, P.imgs, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
                 if (!done) depth++;
             }
             if (done) {
@@ -1214,7 +1221,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
         if (mode == MODE_SHADE) {
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            if (shade(&P, prims, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED) {
+            if (shade(&P, prims, P.mats, P.imgs, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED) {
                 next_sample(contrib);
             } else if (++depth >= P.max_depth) {
                 next_sample(mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
@@ -1668,6 +1675,21 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
     if (node == RW::kSentinel && leaf == 0u) c.mode = MODE_SHADE;
 }
 
+// Diagnostic ray dump (COUNT_TESTS builds of v3): the lanes with `want` append their ray (one atomic per wave).
+__device__ __forceinline__ void dump_ray(const KParams& P, const bool want, const f3 ro, const f3 rd) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    uint32_t base = 0u;
+    if (__lane_id() == leader) base = atomicAdd(P.ray_dump_count, (uint32_t)__popcll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (want && i < P.ray_dump_cap) {
+        P.ray_dump[2 * (size_t)i] = make_float4(ro.x, ro.y, ro.z, 0.0f);
+        P.ray_dump[2 * (size_t)i + 1] = make_float4(rd.x, rd.y, rd.z, 0.0f);
+    }
+}
+
 // v3 kernel: one wave per workgroup, one 8×8 pixel tile per wave; LDS holds the wave's parked path state
 // and its traversal stacks (P.lds_wave_words words).
 template <bool COUNT_TESTS, int WAVES_PER_SIMD, bool TEX, bool PHILOX = false, bool COMPACT = false, bool WIDE = false>
@@ -1750,7 +1772,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             v3_unpark<COMPACT, false>(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            KParamsC* const q = kparams_reload();
+            bool ended = shade<TEX>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
             if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
@@ -1772,6 +1795,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
                 park[(PK_COL + 2) * 64] = __float_as_uint(col.z);
             } else {
                 v3_start_trace<WIDE>(P.num_nodes, c, rays);
+                if (COUNT_TESTS && P.ray_dump) dump_ray(P, depth == P.ray_dump_depth, ro, rd);
             }
             v3_park<COMPACT, false>(park, rng, col, att, sample, depth, rays);
         }
@@ -1825,6 +1849,67 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     finish_pixel<COUNT_TESTS>(P, pix, state_at(P, pix), rng, col, cnt);
 }
 
+// Closest hit of a batch of rays (rt_trace_rays): v3's traversal (while-while, postponed leaves, the regeneration
+// threshold and leaf-break rules) without the shading — a wave owns `per_wave` consecutive rays of the batch and a
+// lane whose ray is done takes the wave's next one (ballot + mbcnt on a wave-uniform counter).  Rays are
+// (origin, -), (direction, -) float4 pairs; out[i] = (primitive index in the scene's BVH order or -1, t bits).
+// For measuring how ray order changes traversal cost (tools/coherence.py: a frame's bounce-2 rays in generation
+// order and sorted), and as a closest-hit query for callers that shade on their own.
+template <bool COUNT_TESTS>
+__global__ __launch_bounds__(64, 8) void trace_rays_kernel(const KParams P, const float4* __restrict__ rays,
+                                                          const uint32_t n_rays, const uint32_t per_wave,
+                                                          int2* __restrict__ out) {
+    using Entry = uint16_t;
+    extern __shared__ float4 lds[];
+    const uint32_t lane = threadIdx.x & 63u;
+    Entry* const stk = reinterpret_cast<Entry*>(lds) + lane;
+    const __amdgpu_buffer_rsrc_t nrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)P.nodes48, (short)0, (int)(P.num_nodes * 48u), 0x00020000);
+    stk[0] = (Entry)RefW<false>::kSentinel;
+    stk[64] = (Entry)RefW<false>::kSentinel;
+    const uint32_t base = blockIdx.x * per_wave;
+    const uint32_t end = min(base + per_wave, n_rays);
+    Counts cnt{0, 0, 0, 0, 0, 0, 0};
+    Cursor c{(int)RefW<false>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_DONE};
+    uint32_t ray = base + lane, nrays = 0u;
+    f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
+    const auto start = [&](uint32_t i) {
+        const float4 o = rays[2 * (size_t)i], d = rays[2 * (size_t)i + 1];
+        ro = xyz(o);
+        rd = xyz(d);
+        v3_start_trace<false>(P.num_nodes, c, nrays);
+    };
+    if (ray < end) start(ray);
+    uint32_t next = base + 64u;  // wave-uniform
+    while (__ballot(c.mode != MODE_DONE) != 0) {
+        if (c.mode == MODE_TRAV) {
+            uint32_t thr = P.regen_threshold;
+            if (P.regen_live_frac) thr = min(thr, ((uint32_t)__popcll(__ballot(c.mode != MODE_DONE)) * P.regen_live_frac) >> 6);
+            v3_traverse<COUNT_TESTS, NODES_48, 0u, false>(nrsrc, P.nodes48, P.refs, P.prims, stk, thr, ro, rd, c, cnt, 64u,
+                                                           P.leaf_break);
+        }
+        if (c.mode == MODE_SHADE) {
+            out[ray] = make_int2(c.hit, __float_as_int(c.t_best));
+            c.mode = MODE_NEED;
+        }
+        const uint64_t needm = __ballot(c.mode == MODE_NEED);
+        if (needm != 0) {
+            const uint32_t i = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+            next += (uint32_t)__popcll(needm);
+            if (c.mode == MODE_NEED) {
+                if (i < end) {
+                    ray = i;
+                    start(i);
+                } else {
+                    c.mode = MODE_DONE;
+                }
+            }
+        }
+    }
+    cnt.rays = nrays;
+    flush_counts<COUNT_TESTS>(P, cnt);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // v4: v3 made persistent, with per-lane pixel regeneration.
 //   v3 gives each lane one pixel for the wave's lifetime, so a lane whose 64 samples are done idles
@@ -1844,7 +1929,8 @@ enum ParkSlotV4 { PK_X = PK_WORDS, PK_G = PK_WORDS + 1, PK_PIX = PK_WORDS + 2, P
 // Work index → pixel of the local image (8×8 tiles, row-major tile order); false when the index lies
 // outside the image or outside the rendered grid.
 __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint32_t& x, uint32_t& g, uint32_t& pix) {
-    const uint32_t tile = idx >> 6, l = idx & 63u;
+    const uint32_t slot = idx >> 6, l = idx & 63u;
+    const uint32_t tile = P.tile_order ? P.tile_order[slot] : slot;
     const uint32_t by = tile / P.tiles_x, bx = tile - by * P.tiles_x;
     x = bx * 8u + (l & 7u);
     const uint32_t ly = by * 8u + (l >> 3);
@@ -1926,7 +2012,7 @@ struct PixelQueue {
                 uint32_t x, g, pix;
                 if (work_pixel(P, wq_next + rank, x, g, pix)) {
                     need = false;
-                    start(x, g, pix);
+                    start(x, g, pix, wq_next + rank);
                 }
             }
             const uint32_t taken = min((uint32_t)__popcll(needm), avail);
@@ -1940,7 +2026,7 @@ struct PixelQueue {
 };
 
 // Wave trace of the persistent kernels (rt_set_wave_trace; tools/v4_timeline.py), kWaveTraceWords words per wave:
-// [0] start, [1] queue found empty, [2] end, [3] pixels taken, [4] HW_REG_HW_ID | HW_REG_XCC_ID << 32 (the wave's
+// [0] start, [1] queue found empty, [2] end, [3] pixels taken | grid waves << 32, [4] HW_REG_HW_ID | HW_REG_XCC_ID << 32 (the wave's
 // SIMD / CU / shader engine and XCD), [5] when it last handed out a pixel, [6] chunk grabs | exhausted-head probes
 // << 32, [7] realtime ticks spent waiting for the queue's atomics.  Times: s_memrealtime (100 MHz).
 constexpr uint32_t kWaveTraceWords = 8;
@@ -1950,7 +2036,7 @@ __device__ __forceinline__ void trace_persistent_wave(const KParams& P, const Pi
         w[0] = rt_start;
         w[1] = queue.rt_drained;
         w[2] = __builtin_amdgcn_s_memrealtime();
-        w[3] = queue.wave_pixels;
+        w[3] = queue.wave_pixels | ((unsigned long long)gridDim.x << 32);
         w[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
         w[5] = queue.rt_last;
@@ -1995,7 +2081,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
             v3_unpark(park, rng, col, att, sample, depth, rays);
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            bool ended = shade<TEX>(kparams_reload(), prims, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+            KParamsC* const q = kparams_reload();
+            bool ended = shade<TEX>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
             if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
@@ -2017,7 +2104,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
         bool need = fin || c.mode == MODE_NEED;
         if (__ballot(need) != 0) {
             if (!shading && need) rays = park[PK_RAYS * 64];
-            queue.take(P, need, [&](uint32_t x, uint32_t g, uint32_t pix) {
+            queue.take(P, need, [&](uint32_t x, uint32_t g, uint32_t pix, uint32_t) {
                 park[PK_X * 64] = x;
                 park[PK_G * 64] = g;
                 park[PK_PIX * 64] = pix;
@@ -2362,7 +2449,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
         if (mode == MODE_SHADE) {
             if (COUNT_TESTS) cnt.wshade += wave_leader();
             f3 contrib;
-            const int res = shade<TEX, true>(kparams_reload(), prims, hit, tag, t, ro, rd, att, rng, rtl, contrib);
+            KParamsC* const q = kparams_reload();
+            const int res = shade<TEX, true>(q, prims, q->mats, q->imgs, hit, tag, t, ro, rd, att, rng, rtl, contrib);
             if (res == SHADE_ENDED) {
                 end_path(contrib);
             } else if (res == SHADE_CONTINUE) {
@@ -2436,10 +2524,30 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     const float4* __restrict__ prims = P.prims;  // the flat table (rt_render)
     const bool rtl = P.rius_rtl != 0;
     const bool accumulate = (P.flags & RT_FLAG_ACCUMULATE) != 0;
+    // The scene's per-lane-indexed tables — the hit primitive's record and reference box, the materials, the image
+    // descriptors: under 8 KB for a flat scene (rt_render checks flat_lds_bytes) — staged in LDS once per persistent
+    // wave: a pass's dependent loads (box check, material, image descriptor before the texel gather) become LDS reads
+    // instead of L2 round trips.  The scan itself keeps its wave-uniform scalar loads of `prims`.
+    extern __shared__ float4 lds_tabs[];
+    float4* const tprims = lds_tabs;
+    float4* const tboxes = tprims + 2u * P.num_prims;
+    float4* const tmats = tboxes + 2u * P.num_prims;
+    int4* const timgs = reinterpret_cast<int4*>(tmats + 3u * P.num_mats);
+    {
+        const uint32_t lane = threadIdx.x & 63u;
+        for (uint32_t i = lane; i < 2u * P.num_prims; i += 64u) {
+            tprims[i] = prims[i];
+            tboxes[i] = P.flat_boxes[i];
+        }
+        for (uint32_t i = lane; i < 3u * P.num_mats; i += 64u) tmats[i] = P.mats[i];
+        for (uint32_t i = lane; i < P.num_imgs; i += 64u) timgs[i] = P.imgs[i];
+        __syncthreads();
+    }
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     R rng{};
     Rng nrng{};               // kNext: the prefetched pixel's state (loads in flight until it starts)
-    uint32_t npix = kNone, nx = 0u, ng = 0u;
+    uint32_t npix = kNone, nx = 0u, ng = 0u, nwidx = 0u;
+    uint32_t widx = 0u, life = 0u;  // the pixel's work index and the passes it has taken (P.pixel_cost)
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // kAcc: the current pixel's accumulator
     f3 col = mk(0.0f, 0.0f, 0.0f), att = col, ro = col, rd = col;
     uint32_t x = 0u, g = 0u, pix = 0u, sample = 0u, depth = 0u, rays = 0u;
@@ -2449,17 +2557,39 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     float t = FLT_MAX;
     PixelQueue queue(blockIdx.x % kQueueCounters);
     const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+    // pass trace (diagnostic, tools/c5_tail.py): every 64th wave stamps each of its first kPassTrace / 4 passes with 4
+    // words: s_memrealtime at the pass start (bits 0-39) with the lanes about to trace (40-46), shade (47-53) and with a
+    // pixel at all (54-60); then s_memrealtime after the trace, after the shading and after the queue
+    constexpr uint32_t kPassTrace = 1024;
+    const bool pass_traced = P.wave_trace && (blockIdx.x & 63u) == 0u &&
+                             (uint64_t)P.wave_trace_words >= (uint64_t)kWaveTraceWords * gridDim.x +
+                                 (uint64_t)kPassTrace * (blockIdx.x / 64u + 1u);
+    unsigned long long* const pass_rec =
+        pass_traced ? P.wave_trace + (size_t)kWaveTraceWords * gridDim.x + (size_t)kPassTrace * (blockIdx.x / 64u) : nullptr;
+    uint32_t pass_no = 0u;
     while (true) {
+        life++;
+        if (pass_traced) {
+            const uint64_t tr = __builtin_amdgcn_s_memrealtime() & 0xffffffffffull;
+            const uint64_t n_t = (uint64_t)__popcll(__ballot(mode == MODE_TRAV));
+            const uint64_t n_s = (uint64_t)__popcll(__ballot(mode == MODE_SHADE));
+            const uint64_t n_a = (uint64_t)__popcll(__ballot(mode == MODE_TRAV || mode == MODE_SHADE));
+            if (4u * pass_no < kPassTrace && wave_leader()) pass_rec[4u * pass_no] = tr | (n_t << 40) | (n_s << 47) | (n_a << 54);
+        }
+        const auto pass_stamp = [&](uint32_t k) {
+            if (pass_traced && 4u * pass_no < kPassTrace && wave_leader()) pass_rec[4u * pass_no + k] = __builtin_amdgcn_s_memrealtime();
+        };
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
-            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.flat_boxes, P.num_prims, ro, rd, hit, tag, t, cnt);
+            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, tboxes, P.num_prims, ro, rd, hit, tag, t, cnt);
             mode = MODE_SHADE;
         }
+        pass_stamp(1);
         bool cam = false;
         if (mode == MODE_SHADE) {
             if (COUNT_TESTS) cnt.wshade += wave_leader();
             f3 contrib;
-            const int res = shade<TEX, true>(kparams_reload(), prims, hit, tag, t, ro, rd, att, rng, rtl, contrib);
+            const int res = shade<TEX, true>(kparams_reload(), tprims, tmats, timgs, hit, tag, t, ro, rd, att, rng, rtl, contrib);
             bool ended = res == SHADE_ENDED;
             if (res == SHADE_CONTINUE && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
@@ -2471,20 +2601,24 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
                     cam = true;
                 } else {  // the pixel is done (Kernel.cu:149-157)
                     write_pixel(P, pix, state_at(P, pix), rng, col, kAcc && accumulate ? &acc : nullptr);
+                    if (P.pixel_cost) P.pixel_cost[widx] = (uint8_t)min(life, 255u);
                     mode = MODE_NEED;
                 }
             } else if (res == SHADE_CONTINUE) {
                 mode = MODE_TRAV;
             }
         }
+        pass_stamp(2);
         // pixel regeneration: a lane without a pixel starts its prefetched one, or takes the next work index
         bool need = mode == MODE_NEED;
         if (__ballot(need) != 0) {
             bool started = false;
-            const auto start = [&](uint32_t sx, uint32_t sg, uint32_t spix, const R& srng) {
+            const auto start = [&](uint32_t sx, uint32_t sg, uint32_t spix, uint32_t swidx, const R& srng) {
                 x = sx;
                 g = sg;
                 pix = spix;
+                widx = swidx;
+                life = 0u;
                 rng = srng;
                 if (kAcc && accumulate && !(P.flags & RT_FLAG_ACCUMULATE_RESET)) acc = P.accum[spix];
                 col = mk(0.0f, 0.0f, 0.0f);
@@ -2495,25 +2629,28 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
             if constexpr (kNext) {
                 if (need && npix != kNone) {
                     need = false;
-                    start(nx, ng, npix, nrng);
+                    start(nx, ng, npix, nwidx, nrng);
                     npix = kNone;
                 }
             }
-            queue.take(P, need, [&](uint32_t qx, uint32_t qg, uint32_t qpix) {  // Kernel.cu:119-123
-                start(qx, qg, qpix, begin_rng<R>(state_at(P, qpix), P.state_stride, qg * P.width + qx));
+            queue.take(P, need, [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {  // Kernel.cu:119-123
+                start(qx, qg, qpix, qidx, begin_rng<R>(state_at(P, qpix), P.state_stride, qg * P.width + qx));
             });
             if (need) mode = MODE_DONE;
             if constexpr (kNext) {  // the next pixel of every lane that just started one: its state loads go out now
                 bool want = started && npix == kNone && queue.head_left > P.work_per_counter / kPrefetchStop;
                 if (__ballot(want) != 0)
-                    queue.take(P, want, [&](uint32_t qx, uint32_t qg, uint32_t qpix) {
+                    queue.take(P, want, [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {
                         nx = qx;
                         ng = qg;
                         npix = qpix;
+                        nwidx = qidx;
                         nrng = load_rng(state_at(P, qpix), P.state_stride);
                     });
             }
         }
+        pass_stamp(3);
+        pass_no++;
         if (cam) {  // next sample's camera ray (Kernel.cu:139-146)
             KParamsC* q = kparams_reload();
             camera_ray(q, lane_camera(q, x, g), rng, ro, rd, sample);
@@ -2722,6 +2859,11 @@ thread_local int g_regen_threshold = 56;
 thread_local int g_lds_pad = 0;  // diagnostic: extra LDS bytes per wave (occupancy experiments)
 thread_local unsigned long long* g_wave_trace = nullptr;  // diagnostic: rt_set_wave_trace
 thread_local unsigned long long g_wave_trace_words = 0;
+thread_local uint8_t* g_pixel_cost = nullptr;  // diagnostic: rt_set_pixel_cost
+thread_local float4* g_ray_dump = nullptr;     // diagnostic: rt_set_ray_dump
+thread_local uint32_t* g_ray_dump_count = nullptr;
+thread_local uint32_t g_ray_dump_cap = 0, g_ray_dump_depth = 1;
+thread_local uint64_t g_pixel_cost_bytes = 0;
 thread_local const uint32_t* g_tile_order = nullptr;       // experiment: rt_set_tile_order
 thread_local int g_adaptive_order = 1;                      // RT_TUNE_ADAPTIVE_ORDER
 // RT_TUNE_REGEN_LIVE_FRAC: v3's regeneration threshold is capped at 48/64 of the wave's live pixels, so a wave whose
@@ -2827,6 +2969,7 @@ int acquire_plan(const PlanKey& key, hipStream_t s, std::shared_ptr<TilePlan>* o
 thread_local int g_persistent_waves = 0;  // 0: occupancy query
 
 constexpr size_t kLdsLimit = 160 * 1024;
+constexpr size_t kFlatTabLdsMax = 16 * 1024;  // LDS per persistent flat wave for the scene tables (64 primitives: 4 KB)
 
 // Work-queue heads of the persistent kernel: a ring of counters per device, one slot per launch, zeroed
 // on the launch's stream right before it.  A slot holds the kQueueCounters heads RT_TUNE_QUEUE_STRIDE apart
@@ -2894,6 +3037,58 @@ extern "C" {
 int rt_set_wave_trace(void* buffer, uint64_t words) {
     g_wave_trace = (unsigned long long*)buffer;
     g_wave_trace_words = buffer ? words : 0;
+    return RT_OK;
+}
+
+int rt_set_ray_dump(void* rays, uint32_t capacity, uint32_t* count, uint32_t depth) {
+    if (rays && (!count || capacity == 0)) {
+        set_error("rt_set_ray_dump: a ray buffer needs a count word and a capacity");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    g_ray_dump = (float4*)rays;
+    g_ray_dump_count = rays ? count : nullptr;
+    g_ray_dump_cap = rays ? capacity : 0u;
+    g_ray_dump_depth = depth;
+    return RT_OK;
+}
+
+int rt_trace_rays(const rt_scene* scene, const float* rays, uint32_t n, int32_t* hits, uint64_t* counters,
+                  int count_tests, rt_stream stream) {
+    if (!scene || (n && (!rays || !hits))) { set_error("rt_trace_rays: NULL argument"); return RT_ERR_INVALID_ARGUMENT; }
+    if (n == 0) return RT_OK;
+    const DeviceScene& S = scene->dev;
+    if (S.wide_refs) { set_error("rt_trace_rays: scenes with 32-bit references are not supported"); return RT_ERR_UNSUPPORTED; }
+    const size_t lds = (size_t)(S.depth + 2) * 64 * 2;
+    if (S.depth > (uint32_t)dev::kStackMax || lds > kLdsLimit) { set_error("rt_trace_rays: BVH too deep"); return RT_ERR_UNSUPPORTED; }
+    dev::KParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.nodes48 = (const float4*)S.nodes48;
+    P.refs = (const uint32_t*)S.refs;
+    P.prims = (const float4*)S.prims;
+    P.num_nodes = S.num_nodes;
+    P.num_prims = S.num_prims;
+    P.counters = (unsigned long long*)counters;
+    P.regen_threshold = (uint32_t)g_regen_threshold;
+    P.regen_live_frac = (uint32_t)g_regen_live_frac;
+    P.leaf_break = (uint32_t)g_leaf_break;
+    // rays per wave: enough waves to fill the device (8 per SIMD), at most 16 rays per lane
+    const uint32_t per_lane = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(16, (uint64_t)n / (64ull * 8192ull)));
+    const uint32_t per_wave = 64u * per_lane;
+    const uint32_t grid = (uint32_t)(((uint64_t)n + per_wave - 1) / per_wave);
+    hipStream_t s = (hipStream_t)stream;
+    (void)hipGetLastError();
+    if (count_tests && counters)
+        hipLaunchKernelGGL(dev::trace_rays_kernel<true>, dim3(grid), dim3(64), lds, s, P, (const float4*)rays, n, per_wave,
+                           (int2*)hits);
+    else
+        hipLaunchKernelGGL(dev::trace_rays_kernel<false>, dim3(grid), dim3(64), lds, s, P, (const float4*)rays, n, per_wave,
+                           (int2*)hits);
+    return hip_check(hipGetLastError(), "rt_trace_rays: kernel launch", RT_ERR_LAUNCH);
+}
+
+int rt_set_pixel_cost(void* buffer, uint64_t bytes) {
+    g_pixel_cost = (bytes && buffer) ? (uint8_t*)buffer : nullptr;
+    g_pixel_cost_bytes = g_pixel_cost ? bytes : 0;
     return RT_OK;
 }
 
@@ -3102,6 +3297,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.counters = (unsigned long long*)a->counters;
     P.num_nodes = S.num_nodes;
     P.num_prims = S.num_prims;
+    P.num_mats = S.num_mats;
+    P.num_imgs = S.num_imgs;
     P.width = a->width;
     P.height = a->height;
     P.spp = a->samples_per_pixel;
@@ -3125,6 +3322,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.wave_trace = g_wave_trace;
     P.wave_trace_words = g_wave_trace_words;
     P.tile_order = g_tile_order;
+    P.ray_dump = g_ray_dump;
+    P.ray_dump_count = g_ray_dump_count;
+    P.ray_dump_cap = g_ray_dump_cap;
+    P.ray_dump_depth = g_ray_dump_depth;
     // Launch-uniform camera terms, with the binary32 operations of Kernel.cu:130-143.
     const rt_input_struct& in = a->inputs;
     P.width_f = (float)a->width;
@@ -3220,7 +3421,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool packable =
         a->samples_per_pixel < 8192u && a->max_depth < 64u && (uint64_t)a->samples_per_pixel * a->max_depth < 8192u;
     if (variant == kVarFlat && !S.prims_flat) variant = kVarV3Compact;  // (a scene beyond kFlatMaxPrims)
-    if (variant == kVarFlatPersistent && !S.prims_flat) variant = kVarV4;
+    // the persistent flat kernel stages the flat tables in LDS: a scene whose materials overflow kFlatTabLdsMax runs v4
+    const size_t flat_tab_bytes = ((size_t)4 * S.num_prims + (size_t)3 * S.num_mats + S.num_imgs) * 16u;
+    if (variant == kVarFlatPersistent && (!S.prims_flat || flat_tab_bytes > kFlatTabLdsMax)) variant = kVarV4;
     if (kVariants[variant].compact && !packable) variant = kVarV3;  // packed counters would overflow
     if ((kVariants[variant].kernel == 4 || kVariants[variant].kernel == 6) && (a->samples_per_pixel == 0 || a->max_depth == 0))
         variant = kVariants[variant].kernel == 6 ? kVarFlat  // the persistent kernels assume every pixel traces a ray
@@ -3258,7 +3461,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                                         (size_t)(S.depth + 2) * 64 * (wide ? 4 : 2) + (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
-    size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes;
+    size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes +
+                       (V.kernel == 6 ? flat_tab_bytes : 0);
     if (lds_bytes > kLdsLimit) {
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
@@ -3284,6 +3488,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                            "rt_render: occupancy query");
         if (rc != RT_OK) return rc;
         P.work_total = tiles * 64u;
+        P.pixel_cost = g_pixel_cost_bytes >= (uint64_t)P.work_total ? g_pixel_cost : nullptr;
         P.work_chunk = (uint32_t)g_queue_chunk;
         P.queue_stride = (uint32_t)g_queue_stride / 4u;
         P.work_per_counter = (tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;

@@ -22,6 +22,7 @@ struct DeviceScene {
     const void* imgs = nullptr;    // int4 per image
     const void* texels = nullptr;  // RGB8
     uint32_t num_nodes = 0, num_prims = 0, num_mats = 0, depth = 0;
+    uint32_t num_imgs = 0;  // image descriptors (int4 each)
     bool has_image_textures = false;
     bool has_textures = false;  // any CHECKER or IMAGE albedo (selects the texture-capable kernel)
     uint64_t device_bytes = 0;

@@ -311,8 +311,28 @@ float rt_last_launch_host_ms(void);
 int rt_set_wave_trace(void* buffer, uint64_t words);
 
 /* Experiment (per thread): device uint32 permutation of the frame's 8×8 tiles giving the v3 kernels' launch
- * order (NULL = row-major).  Results do not depend on it (every pixel is independent); the time does. */
+ * order, and the order the persistent kernels' work queue hands tiles out in (NULL = row-major).  Results do not
+ * depend on it (every pixel is independent); the time does. */
 int rt_set_tile_order(const void* order);
+
+/* Diagnostic (per thread): device buffer of `bytes` uint8 that later persistent-flat launches fill, per work index
+ * (tile slot · 64 + pixel of the 8×8 tile), with the loop passes the pixel took (clamped at 255) — the cost
+ * measure a cost-ordered queue plans from.  Ignored when smaller than the frame's work indices.  NULL = off. */
+int rt_set_pixel_cost(void* buffer, uint64_t bytes);
+
+/* Diagnostic (per thread): later rt_render calls with RT_FLAG_COUNT_TESTS on the v3 kernels (variants 2, 3) append
+ * every ray that starts at bounce `depth` (1 = the first scattered ray; 0 is not recorded) to `rays` as (origin, 0),
+ * (direction, 0) float4 pairs, up to `capacity` rays; *count (device uint32, caller-zeroed) counts the rays offered,
+ * so min(*count, capacity) were written.  rays = NULL: off.  (tools/coherence.py) */
+int rt_set_ray_dump(void* rays, uint32_t capacity, uint32_t* count, uint32_t depth);
+
+/* Closest hit of n rays (device (origin, -), (direction, -) float4 pairs) against the scene, with v3's traversal
+ * (BVHNode::Hit semantics, Hittable.cuh:387-439; t in (0.001, FLT_MAX)): hits[2i] = the primitive's index in the
+ * scene's BVH order or -1, hits[2i + 1] = the hit distance's bits.  counters: optional device uint64[RT_COUNTERS_WORDS]
+ * ([0] rays; with count_tests also box and primitive tests and wave iterations, as rt_render).  Asynchronous on
+ * `stream`.  Scenes with 32-bit references are not supported (RT_ERR_UNSUPPORTED). */
+int rt_trace_rays(const rt_scene* scene, const float* rays, uint32_t n, int32_t* hits, uint64_t* counters,
+                  int count_tests, rt_stream stream);
 
 /* Tuning/benchmark knob (per thread): the kernel rt_render launches.  -1 = automatic: 3 from 64 spp; below,
  * the faster of 3 and 4 as timed on the first frames of each (device, stream, scene, frame shape, spp, depth,

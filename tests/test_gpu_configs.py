@@ -463,7 +463,7 @@ def test_persistent_wave_trace_accounts_for_every_pixel(variant, c5_scene):
     cfg = scenes.CONFIGS["c5"].scaled(256, 128)
     ds = DeviceScene(c5_scene)
     lib().rt_set_variant(variant)
-    trace = torch.zeros(8 * 8192, dtype=torch.int64, device="cuda")
+    trace = torch.zeros(8 * 600, dtype=torch.int64, device="cuda")  # the per-wave records only (no pass records)
     imgs = []
     try:
         for traced in (False, True):
@@ -479,7 +479,8 @@ def test_persistent_wave_trace_accounts_for_every_pixel(variant, c5_scene):
     np.testing.assert_array_equal(imgs[0], imgs[1])
     t = trace.cpu().numpy().view(np.uint64).reshape(-1, 8)
     t = t[t[:, 0] > 0]
-    assert int(t[:, 3].sum()) == cfg.width * cfg.height
+    assert int((t[:, 3] & 0xFFFFFFFF).sum()) == cfg.width * cfg.height
+    assert np.all((t[:, 3] >> 32) == len(t))  # every wave of the grid wrote its record
     assert np.all(t[:, 2] >= t[:, 0])
     xcc = (t[:, 4] >> 32) & 0xF
     assert set(np.unique(xcc).tolist()) <= set(range(8))

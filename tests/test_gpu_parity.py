@@ -901,3 +901,48 @@ def test_v3_scheduling_knobs_change_schedule_not_pixels(key, value, variant):
     finally:
         lib().rt_set_tuning(key, prev)
         lib().rt_set_variant(-1)
+
+
+def test_trace_rays_matches_brute_force_closest_hit():
+    """rt_trace_rays (v3's traversal without shading, tools/coherence.py) returns each ray's closest hit: against a
+    numpy brute force over RTIOW's 488 spheres with Sphere::Hit's binary32 operations (Hittable.cuh:80-110: near
+    root, else far root, strictly inside (0.001, FLT_MAX)), the hit distances are equal bit for bit, in any ray order."""
+    sc = scenes.builtin(scenes.CONFIGS["c2"].scene)
+    ds = DeviceScene(sc)
+    rng = np.random.default_rng(5)
+    n = 8192
+    o = np.stack([rng.uniform(-12, 12, n), rng.uniform(0.05, 3.0, n), rng.uniform(-12, 12, n)], 1).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[: n // 4, 1] = -np.abs(d[: n // 4, 1])  # a quarter aimed down at the small spheres and the ground
+    rays = np.zeros((2 * n, 4), np.float32)
+    rays[0::2, :3], rays[1::2, :3] = o, d
+    # brute force (float32 throughout, the kernel's operation order)
+    c = np.array([list(h.center) for h in sc.hittables], np.float32)
+    r2 = np.array([h.radius * h.radius for h in sc.hittables], np.float32)
+    f = np.float32
+    best = np.full(n, np.inf, np.float32)
+    a = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+    for k in range(len(c)):
+        oc = o - c[k]
+        b = (oc[:, 0] * d[:, 0] + oc[:, 1] * d[:, 1]) + oc[:, 2] * d[:, 2]
+        cc = ((oc[:, 0] * oc[:, 0] + oc[:, 1] * oc[:, 1]) + oc[:, 2] * oc[:, 2]) - r2[k]
+        disc = b * b - a * cc
+        with np.errstate(invalid="ignore"):
+            sq = np.sqrt(np.where(disc > 0, disc, f(1.0)))
+            tn, tf = (-b - sq) / a, (-b + sq) / a
+        t = np.where(tn > f(0.001), tn, np.where(tf > f(0.001), tf, np.inf)).astype(np.float32)
+        t = np.where(disc > 0, t, np.inf)
+        best = np.minimum(best, t)
+    for perm in (np.arange(n), rng.permutation(n)):
+        dr = torch.from_numpy(np.ascontiguousarray(rays.reshape(n, 8)[perm].reshape(2 * n, 4))).cuda()
+        hits = torch.empty(2 * n, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(abi.COUNTERS_WORDS, dtype=torch.int64, device="cuda")
+        assert lib().rt_trace_rays(ds.handle, C.c_void_p(dr.data_ptr()), n, C.c_void_p(hits.data_ptr()),
+                                   C.c_void_p(cnt.data_ptr()), 1, None) == 0
+        torch.cuda.synchronize()
+        h = hits.cpu().numpy().reshape(n, 2)
+        got = np.where(h[:, 0] >= 0, h[:, 1].view(np.float32), np.inf)
+        want = best[perm]
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+        assert int(cnt[0]) == n and int(cnt[1]) > 2 * n
+    assert np.isfinite(best).mean() > 0.3
