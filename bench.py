@@ -528,11 +528,12 @@ def valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world) -> dict:
 
 def hbm_roofline(args, cfg, r, c, kernel_ms) -> dict:
     """C5 is the one configuration whose frame moves HBM bytes worth a roofline: per pixel
-    the RNG state in and out (24 + 24 B used, either layout; none for Philox), the float4 accumulator read and
-    written (32 B) and the RGBA8 store (4 B).  The texel gathers (3 B per image-texture lookup, at most one per
-    ray) are not in the algorithmic figure; the PMC traffic includes them."""
+    the RNG state in and out (24 + 24 B used, either layout; none for Philox), the float4 accumulator written (16 B:
+    the scripted camera moves every frame, so every frame restarts the accumulation with RT_FLAG_ACCUMULATE_RESET,
+    which writes it without reading it) and the RGBA8 store (4 B).  The texel gathers (3 B per image-texture lookup,
+    at most one per ray) are not in the algorithmic figure; the PMC traffic includes them."""
     px = cfg.width * r.local_rows
-    per_px = (0 if args.rng == "philox" else 48) + 32 + 4
+    per_px = (0 if args.rng == "philox" else 48) + 16 + 4
     algo = per_px * px
     achieved = algo / (kernel_ms * 1e-3) / 1e9
     pmc = pmc_profile("c5", args.rng, args.state_layout)

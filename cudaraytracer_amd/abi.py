@@ -29,6 +29,7 @@ RT_TUNE_REGEN_THRESHOLD, RT_TUNE_LEAF_MAX, RT_TUNE_PERSISTENT_WAVES, RT_TUNE_SAH
 RT_TUNE_LDS_PAD, RT_TUNE_ADAPTIVE_ORDER, RT_TUNE_TEXEL_LAYOUT, RT_TUNE_QUEUE_CHUNK = 4, 5, 6, 7
 RT_TUNE_QUEUE_STRIDE, RT_TUNE_REGEN_LIVE_FRAC, RT_TUNE_LEAF_BREAK, RT_TUNE_RIUS_TRIPS = 8, 9, 10, 11
 RT_TUNE_FLAT_MAX = 12
+RT_TUNE_QUEUE_PREFETCH = 13
 
 STATUS = {
     0: "RT_OK",

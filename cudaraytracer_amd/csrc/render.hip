@@ -238,6 +238,7 @@ struct KParams {
                                // (RT_TUNE_QUEUE_CHUNK; a multiple of 64); 64 near the head's end
     uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
     uint32_t work_per_counter; // v4: indices per queue head (a multiple of 64): head k owns [k·n, (k+1)·n)
+    uint32_t queue_prefetch;   // persistent kernels: fetch the next chunk once at most this many indices are left (0: off)
     uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
     uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
     unsigned long long* wave_trace;  // diagnostic: v3 / flat per tile {start, end} of s_memrealtime (100 MHz); the
@@ -1957,7 +1958,14 @@ struct PixelQueue {
     uint64_t rt_last = 0u;                 // (wave trace) when it last handed a pixel to a lane
     uint64_t rt_atomic = 0u;               // (wave trace) realtime ticks spent waiting for queue atomics
     uint32_t n_grab = 0u, n_probe = 0u;    // (wave trace) chunk atomics that returned work / found a head exhausted
+    // The next chunk's atomic, issued ahead (P.queue_prefetch): its result stays in the issuing lane's VGPR until the
+    // current chunk runs out, so its round trip (1-5 us under load, profiles/r05b_c5_tail.txt) overlaps the wave's work
+    bool pf_valid = false;                 // wave-uniform: an atomic on head qc is in flight for the next chunk
+    uint32_t pf_base = 0u, pf_leader = 0u, pf_want = 0u;
     __device__ explicit PixelQueue(uint32_t head) : qc(head) {}
+    __device__ __forceinline__ uint32_t chunk_want(const KParams& P) const {
+        return head_left > 4u * P.work_chunk ? P.work_chunk : 64u;
+    }
     // Lanes with `need` take the next work indices of the wave's chunk (ballot + mbcnt rank); start(x, g, pix) runs on
     // every lane that gets a pixel, and its `need` clears.  A lane still needing one afterwards found the queue empty.
     template <class F>
@@ -1965,12 +1973,19 @@ struct PixelQueue {
         uint64_t needm = __ballot(need);
         while (needm != 0 && !drained) {
             if (wq_next >= wq_end) {
-                const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
-                uint32_t base = 0u;
-                const uint32_t want = head_left > 4u * P.work_chunk ? P.work_chunk : 64u;
+                uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+                uint32_t base = 0u, want;
                 const uint64_t ta = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
-                if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, want);
-                base = __builtin_amdgcn_readlane(base, leader);
+                if (pf_valid) {  // the chunk fetched ahead (same head: qc changes only below, after consuming it)
+                    leader = pf_leader;
+                    want = pf_want;
+                    base = __builtin_amdgcn_readlane(pf_base, leader);
+                    pf_valid = false;
+                } else {
+                    want = chunk_want(P);
+                    if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, want);
+                    base = __builtin_amdgcn_readlane(base, leader);
+                }
                 const uint32_t idx = qc * P.work_per_counter + base;
                 if (P.wave_trace) {  // (diagnostic: the atomic's round trip, stamped after its result is in)
                     __builtin_amdgcn_s_waitcnt(0);
@@ -2022,8 +2037,29 @@ struct PixelQueue {
             wave_pixels += (uint32_t)__popcll(needm & ~still);
             needm = still;
         }
+        // fetch the next chunk ahead once the current one is nearly used up (never after the queue ran dry: a chunk
+        // fetched ahead is always consumed by a later take before the wave can find the queue empty)
+        if (P.queue_prefetch && !drained && !pf_valid && wq_end - wq_next <= P.queue_prefetch) {
+            pf_leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+            pf_want = chunk_want(P);
+            if (__lane_id() == pf_leader) pf_base = atomicAdd(P.work_counter + qc * P.queue_stride, pf_want);
+            pf_valid = true;
+        }
     }
 };
+
+// End of a persistent wave: the grid's last wave to finish zeroes the queue slot (its heads, the exhausted-heads word
+// and the finished-waves count kQueueCounters + 1 strides in), so the slot is clean for the launch that reuses it and
+// rt_render needs no memset per frame (5 us per C5 frame, profiles/r04p_kernel_stats_by_grid_c5.csv).  Every wave
+// reaches this point after its last queue atomic has returned.
+__device__ __forceinline__ void queue_release(const KParams& P) {
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+    uint32_t fin = 0u;
+    if (__lane_id() == leader) fin = atomicAdd(P.work_counter + (kQueueCounters + 1u) * P.queue_stride, 1u);
+    fin = __builtin_amdgcn_readlane(fin, leader);
+    if (fin == gridDim.x - 1u && __lane_id() < kQueueCounters + 2u)
+        __hip_atomic_store(P.work_counter + __lane_id() * P.queue_stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Wave trace of the persistent kernels (rt_set_wave_trace; tools/v4_timeline.py), kWaveTraceWords words per wave:
 // [0] start, [1] queue found empty, [2] end, [3] pixels taken | grid waves << 32, [4] HW_REG_HW_ID | HW_REG_XCC_ID << 32 (the wave's
@@ -2130,6 +2166,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
     cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;
     trace_persistent_wave(P, queue, rt_start);
+    queue_release(P);
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
@@ -2663,6 +2700,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     cnt.rays = rays;
     cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
     trace_persistent_wave(P, queue, rt_start);
+    queue_release(P);
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
@@ -2979,10 +3017,11 @@ constexpr uint32_t kQueueSlots = 256;
 constexpr uint32_t kQueueMaxStride = 4096;  // bytes between heads (RT_TUNE_QUEUE_STRIDE)
 thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's queue heads
 thread_local int g_queue_chunk = 64;    // RT_TUNE_QUEUE_CHUNK: work indices per queue atomic
+thread_local int g_queue_prefetch = 0;  // RT_TUNE_QUEUE_PREFETCH: fetch the next chunk ahead at this many indices left
 constexpr int kMaxDevices = 64;
 struct QueueRing {
     uint32_t* buf = nullptr;
-    size_t slot_bytes = 0;  // (kQueueCounters + 1) heads at the largest stride used so far on the device
+    size_t slot_bytes = 0;  // kQueueCounters heads + the exhausted and finished words at the largest stride used
     std::atomic<uint32_t> next{0};
     int cus = 0;
     std::vector<void*> retired;  // rings outgrown by a larger stride: never freed (see acquire_queue)
@@ -3001,7 +3040,7 @@ int acquire_queue(int device, uint32_t stride, uint32_t** head, int* cus) {
         return RT_ERR_DEVICE;
     }
     QueueRing& q = g_queues[device];
-    const size_t need = (size_t)(dev::kQueueCounters + 1u) * stride;
+    const size_t need = (size_t)(dev::kQueueCounters + 2u) * stride;
     std::lock_guard<std::mutex> lock(g_queue_mu);
     if (!q.buf || q.slot_bytes < need) {
         if (q.buf) {
@@ -3011,6 +3050,13 @@ int acquire_queue(int device, uint32_t stride, uint32_t** head, int* cus) {
         void* p = nullptr;
         int rc = hip_check(hipMalloc(&p, (size_t)kQueueSlots * need), "rt_render: work queue allocation");
         if (rc != RT_OK) return rc;
+        // zeroed once, before any launch can take a slot (every launch leaves its slot zeroed: queue_release)
+        rc = hip_check(hipMemset(p, 0, (size_t)kQueueSlots * need), "rt_render: work queue reset");
+        if (rc == RT_OK) rc = hip_check(hipDeviceSynchronize(), "rt_render: work queue reset");
+        if (rc != RT_OK) {
+            (void)hipFree(p);
+            return rc;
+        }
         q.buf = (uint32_t*)p;
         q.slot_bytes = need;
         if (q.cus == 0) {
@@ -3222,6 +3268,15 @@ int rt_set_tuning(int key, int value) {
         }
         int prev = g_flat_max;
         g_flat_max = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_PREFETCH) {
+        if (value < 0 || value > 64) {
+            set_error("rt_set_tuning: queue prefetch must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_prefetch;
+        g_queue_prefetch = value;
         return prev;
     }
     if (key == RT_TUNE_PERSISTENT_WAVES) {
@@ -3490,6 +3545,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.work_total = tiles * 64u;
         P.pixel_cost = g_pixel_cost_bytes >= (uint64_t)P.work_total ? g_pixel_cost : nullptr;
         P.work_chunk = (uint32_t)g_queue_chunk;
+        P.queue_prefetch = (uint32_t)g_queue_prefetch;
         P.queue_stride = (uint32_t)g_queue_stride / 4u;
         P.work_per_counter = (tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
         // the persistent flat kernel runs 4 waves per SIMD even where its registers allow 5-6: C5 0.294 vs 0.307 ms
@@ -3498,9 +3554,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
         grid = (uint32_t)(resident < grid ? resident : grid);
-        rc = hip_check(hipMemsetAsync(P.work_counter, 0, (size_t)(dev::kQueueCounters + 1u) * g_queue_stride, s),
-                       "rt_render: work queue reset");
-        if (rc != RT_OK) return rc;
+        // (no reset here: the slot is zero, the previous launch that used it left it so, queue_release)
     }
     P.num_tiles = tiles;
     std::shared_ptr<TilePlan> plan;

@@ -376,12 +376,15 @@ int rt_last_variant(void);
  *   reference's only on exact ties and hits within rounding of a reference box face.  RT_TUNE_RIUS_TRIPS: the flat
  *   kernels make at most this many RandomInUnitSphere attempts (Math.cuh:252-260) per shading pass; a lane whose
  *   attempts were all rejected continues the same call at the wave's next pass (0 = unbounded; 0..64; default 4;
- *   Philox mode rounds it up to whole blocks of four attempts).  It does not change the image. */
+ *   Philox mode rounds it up to whole blocks of four attempts).  It does not change the image.
+ *   RT_TUNE_QUEUE_PREFETCH: the persistent kernels (variants 4, 6) fetch their next chunk of work indices (the queue
+ *   atomic) ahead, once at most this many indices of the current chunk are left, so the atomic's round trip overlaps
+ *   the wave's work (0 = off: fetched when the chunk runs out; 0..64).  It does not change the image. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
                      RT_TUNE_REGEN_LIVE_FRAC = 9, RT_TUNE_LEAF_BREAK = 10, RT_TUNE_RIUS_TRIPS = 11,
-                     RT_TUNE_FLAT_MAX = 12 };
+                     RT_TUNE_FLAT_MAX = 12, RT_TUNE_QUEUE_PREFETCH = 13 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

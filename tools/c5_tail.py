@@ -18,18 +18,16 @@ from cudaraytracer_amd._lib import lib
 from cudaraytracer_amd.renderer import DeviceScene, Renderer
 
 WORDS = 8  # kWaveTraceWords (render.hip)
+PASS_WORDS = 1024  # kPassTrace: per-pass stamps of every 64th wave (persistent flat kernel)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--out", default="gpurun_out/c5_tail")
 ap.add_argument("--frames", type=int, default=6)
 ap.add_argument("--variant", type=int, default=6)
-ap.add_argument("--tune", default="", help="k=v,... rt_set_tuning before the cases")
+ap.add_argument("--tune", default="", help="k=v,...[;k=v,...] rt_set_tuning sets: every case runs under each set")
 ap.add_argument("--cases", default="d4,d1,d1p")
 args = ap.parse_args()
 os.makedirs(args.out, exist_ok=True)
-for kv in filter(None, args.tune.split(",")):
-    k, v = (int(x) for x in kv.split("="))
-    lib().rt_set_tuning(k, v)
 
 c5 = scenes.CONFIGS["c5"]
 ds5 = DeviceScene(c5.scene_desc())
@@ -40,12 +38,12 @@ CASES = {"d4": dict(depth=4, flags=ACC, rng="xorwow"),   # as configured
          "d1p": dict(depth=1, flags=0, rng="philox")}    # no state, no accumulator
 
 
-def run(name, depth, flags, rng):
+def run(name, depth, flags, rng, tag=""):
     lib().rt_set_variant(args.variant)
     r = Renderer(c5.width, c5.height, rng=rng, state_layout="soa")
     r.render_init()
     lib().rt_set_timing(1)
-    ms, traces = [], []
+    ms, traces, passes = [], [], []
     for f in range(args.frames + 2):
         pos, fwd = scenes.moving_camera(f, 60)
         inp = scenes.camera_inputs(pos, fwd, c5.fov)
@@ -58,8 +56,11 @@ def run(name, depth, flags, rng):
         lib().rt_set_wave_trace(None, 0)
         if traced:
             ms.append(lib().rt_last_kernel_ms())
-            t = trace.cpu().numpy().reshape(-1, WORDS)
+            full = trace.cpu().numpy()
+            grid = int(full[3]) >> 32  # (wave 0's record: pixels | grid << 32)
+            t = full[:WORDS * grid].reshape(-1, WORDS)
             traces.append(t[t[:, 0] > 0].copy())
+            passes.append(full[WORDS * grid:WORDS * grid + PASS_WORDS * ((grid + 63) // 64)].reshape(-1, PASS_WORDS).copy())
     # untraced frames: the trace's own cost
     plain = []
     for f in range(args.frames):
@@ -74,9 +75,19 @@ def run(name, depth, flags, rng):
     arr = np.zeros((len(traces), n, WORDS), np.uint64)
     for i, t in enumerate(traces):
         arr[i, :len(t)] = t.view(np.uint64)
-    np.savez_compressed(os.path.join(args.out, f"{name}.npz"), trace=arr, ms=np.array(ms), plain_ms=np.array(plain))
-    print(f"{name}: traced {np.median(ms):.3f} ms, untraced {np.median(plain):.3f} ms, waves {n}", flush=True)
+    np.savez_compressed(os.path.join(args.out, f"{name}{tag}.npz"), trace=arr, ms=np.array(ms), plain_ms=np.array(plain),
+                        passes=np.stack(passes).view(np.uint64))
+    wait = arr[:, :, 7].astype(np.float64).sum(axis=1) * 0.01 / np.maximum(1, (arr[:, :, 0] > 0).sum(axis=1))
+    print(f"{name}{tag}: mean atomic wait/wave {np.median(wait):.1f} us, traced {np.median(ms):.3f} ms, untraced {np.median(plain):.3f} ms, waves {n}", flush=True)
 
 
-for name in args.cases.split(","):
-    run(name, **CASES[name])
+for tset in args.tune.split(";"):
+    prev = []
+    for kv in filter(None, tset.split(",")):
+        k, v = (int(x) for x in kv.split("="))
+        prev.append((k, lib().rt_set_tuning(k, v)))
+    tag = ("_" + tset.replace(",", "_").replace("=", "-")) if tset else ""
+    for name in args.cases.split(","):
+        run(name, tag=tag, **CASES[name])
+    for k, v in reversed(prev):
+        lib().rt_set_tuning(k, v)

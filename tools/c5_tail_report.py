@@ -24,7 +24,7 @@ def analyse(path):
     start, dry, end = (t[:, 0] - t0) * TICK_US, (t[:, 1] - t0) * TICK_US, (t[:, 2] - t0) * TICK_US
     dry = np.where(t[:, 1] > 0, dry, end)
     last = np.where(t[:, 5] > 0, (t[:, 5] - t0) * TICK_US, start)
-    px = t[:, 3]
+    px = t[:, 3] & 0xFFFFFFFF
     hw = t[:, 4] & 0xFFFFFFFF
     xcc = (t[:, 4] >> 32) & 0xF
     cu = (hw >> 8) & 0xF
@@ -62,3 +62,46 @@ def analyse(path):
 
 for p in sys.argv[1:]:
     analyse(p)
+
+
+def passes(path):
+    """Per-pass stamps of every 64th wave (persistent flat kernel, 4 words per pass): pass durations split into the
+    trace, the shading, the queue and the camera rays, before and after the wave found the queue dry."""
+    z = np.load(path)
+    if "passes" not in z:
+        return
+    tr, ms, ps = z["trace"].astype(np.int64), z["ms"], z["passes"].astype(np.int64)
+    k = int(np.argsort(ms)[len(ms) // 2])
+    t, p = tr[k], ps[k]
+    t0 = t[t[:, 0] > 0, 0].min() & 0xFFFFFFFFFF
+    rows = {"steady": [], "tail": []}
+    npass = []
+    for i in range(p.shape[0]):
+        w = t[64 * i]
+        rec = p[i].reshape(-1, 4)
+        rec = rec[rec[:, 0] != 0]
+        if len(rec) < 2:
+            continue
+        st = ((rec[:, 0] & 0xFFFFFFFFFF) - t0) * TICK_US
+        a, b, c = ((rec[:, 1] & 0xFFFFFFFFFF) - t0) * TICK_US, ((rec[:, 2] & 0xFFFFFFFFFF) - t0) * TICK_US, \
+            ((rec[:, 3] & 0xFFFFFFFFFF) - t0) * TICK_US
+        nxt = np.append(st[1:], ((w[2] & 0xFFFFFFFFFF) - t0) * TICK_US)
+        act = (rec[:, 0] >> 54) & 0x7F
+        dry = (((w[1] if w[1] > 0 else w[2]) & 0xFFFFFFFFFF) - t0) * TICK_US
+        for q in range(len(rec)):
+            rows["tail" if st[q] >= dry else "steady"].append((nxt[q] - st[q], a[q] - st[q], b[q] - a[q], c[q] - b[q],
+                                                               nxt[q] - c[q], act[q]))
+        npass.append(len(rec))
+    print(f"   sampled waves {len(npass)}, passes/wave p10/50/90 {'/'.join(f'{v:.0f}' for v in np.percentile(npass, [10, 50, 90]))}"
+          "; per pass mean us (median): total | trace | shade | queue | camera+loop | lanes with a pixel")
+    for name, r in rows.items():
+        if not r:
+            continue
+        r = np.array(r)
+        f = lambda j: f"{r[:, j].mean():5.2f} ({np.median(r[:, j]):5.2f})"
+        print(f"     {name:6s} {len(r) / max(1, len(npass)):5.1f} passes/wave: {f(0)} | {f(1)} | {f(2)} | {f(3)} | {f(4)} | "
+              f"{r[:, 5].mean():.1f}")
+
+
+for p in sys.argv[1:]:
+    passes(p)
