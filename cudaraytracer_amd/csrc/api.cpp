@@ -95,6 +95,8 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     if ((rc = upload(h.flat_boxes, &p, "hipMalloc/hipMemcpy(flat_boxes)"))) goto fail;
     d.flat_boxes = p;
     d.touching_rects = h.touching_rects;
+    d.flat_runs[0] = h.flat_runs[0];
+    d.flat_runs[1] = h.flat_runs[1];
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
     d.mats = p;
     if ((rc = upload(h.imgs, &p, "hipMalloc/hipMemcpy(images)"))) goto fail;

@@ -257,6 +257,7 @@ struct KParams {
     uint32_t rius_cap;               // flat: RandomInUnitSphere attempts per shading pass (0xffffffff = unbounded)
     const float4* ref_nodes;         // flat kernel: the reference BVH over the flat table (ref_trace)
     const float4* flat_boxes;        // flat kernel: per flat record its reference box (flat_trace's exactness check)
+    uint32_t flat_runs[2];           // flat kernel: [begin, end) of each primitive type's run in the flat table
 };
 
 constexpr int kStackMax = 64;
@@ -2289,8 +2290,9 @@ __device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, cons
 // scan.  Those rays (about 1e-5 of them) replay the reference exactly (ref_trace); the rest are exact as they stand.
 template <bool COUNT_TESTS>
 __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, const float4* __restrict__ rnodes,
-                                           const float4* __restrict__ boxes, const uint32_t n, const f3 ro,
-                                           const f3 rd, int& hit, uint32_t& tag, float& t_best, Counts& cnt) {
+                                           const float4* __restrict__ boxes, const uint32_t n, const uint32_t runs0,
+                                           const uint32_t runs1, const f3 ro, const f3 rd, int& hit, uint32_t& tag,
+                                           float& t_best, Counts& cnt) {
     hit = -1;
     tag = 0u;
     t_best = FLT_MAX;
@@ -2323,16 +2325,29 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
         hit = acc ? (int)i : hit;
         tag = acc ? __float_as_uint(q1.w) : tag;
     };
-    for (uint32_t i = 0; i < n; i++) {
-        // wave-uniform record: scalar loads through the constant cache
+    // wave-uniform record: scalar loads through the constant cache
+    const auto record = [&](const uint32_t i, float4& q0, float4& q1) {
         const ConstF32* q = (const ConstF32*)((const ConstU8*)prims + i * 32u);
-        const float4 q0 = make_float4(q[0], q[1], q[2], q[3]), q1 = make_float4(q[4], q[5], q[6], q[7]);
-        const uint32_t type = __float_as_uint(q1.w) & 15u;
-        if (COUNT_TESTS) {
-            cnt.prims++;
-            cnt.rects += type != RT_SPHERE ? 1u : 0u;
-        }
-        if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+        q0 = make_float4(q[0], q[1], q[2], q[3]);
+        q1 = make_float4(q[4], q[5], q[6], q[7]);
+        if (COUNT_TESTS) cnt.prims++;
+    };
+    // One primitive type at a time: prims_flat keeps each type as one contiguous run (scene_build.cpp, `runs`: [begin,
+    // end) of type t in bytes 2t, 2t + 1), so no test sits behind a per-primitive type branch (whose merges cost ~8
+    // register copies per rectangle).  The scan order does not change the answer: without a tie the closest hit is the
+    // unique minimum, and a tie at the minimum is flagged in whichever order its primitives come (the second one seen
+    // either ties t_best or, for a rectangle, re-accepts it), then replayed below.
+    const auto run = [&](const int t, uint32_t& b, uint32_t& e) {
+        const uint32_t v = (t < 2 ? runs0 : runs1) >> (16 * (t & 1));
+        b = v & 0xffu;
+        e = (v >> 8) & 0xffu;
+    };
+    uint32_t rb, re;
+    run(RT_SPHERE, rb, re);
+    for (uint32_t i = rb; i < re; i++) {
+        float4 q0, q1;
+        record(i, q0, q1);
+        {  // Sphere::Hit (Hittable.cuh:80-110)
             const f3 oc = sub(ro, xyz(q0));
             const float b = dot(oc, rd);
             const float c = dot(oc, oc) - q1.x;
@@ -2348,13 +2363,28 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
             t_best = acc ? t : t_best;
             hit = acc ? (int)i : hit;
             tag = acc ? __float_as_uint(q1.w) : tag;
-        } else if (type == RT_XYRECT) {
-            rect(q0, q1, i, ro.z, iz, ro.x, rd.x, ro.y, rd.y);
-        } else if (type == RT_XZRECT) {
-            rect(q0, q1, i, ro.y, iy, ro.x, rd.x, ro.z, rd.z);
-        } else {  // YZRect: y from the height, z from the width (Hittable.cuh:255-258)
-            rect(q0, q1, i, ro.x, ix, ro.y, rd.y, ro.z, rd.z);
         }
+    }
+    run(RT_XYRECT, rb, re);
+    for (uint32_t i = rb; i < re; i++) {
+        float4 q0, q1;
+        record(i, q0, q1);
+        if (COUNT_TESTS) cnt.rects++;
+        rect(q0, q1, i, ro.z, iz, ro.x, rd.x, ro.y, rd.y);
+    }
+    run(RT_XZRECT, rb, re);
+    for (uint32_t i = rb; i < re; i++) {
+        float4 q0, q1;
+        record(i, q0, q1);
+        if (COUNT_TESTS) cnt.rects++;
+        rect(q0, q1, i, ro.y, iy, ro.x, rd.x, ro.z, rd.z);
+    }
+    run(RT_YZRECT, rb, re);
+    for (uint32_t i = rb; i < re; i++) {  // YZRect: y from the height, z from the width (Hittable.cuh:255-258)
+        float4 q0, q1;
+        record(i, q0, q1);
+        if (COUNT_TESTS) cnt.rects++;
+        rect(q0, q1, i, ro.x, ix, ro.y, rd.y, ro.z, rd.z);
     }
     // (a): p*'s hit point against the faces of p*'s own reference box (boxes: scene_build.cpp pack_flat_box)
     bool edge = false;
@@ -2478,7 +2508,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
         }
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
-            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.flat_boxes, P.num_prims, ro, rd, hit, tag, t, cnt);
+            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.flat_boxes, P.num_prims, P.flat_runs[0], P.flat_runs[1], ro, rd, hit,
+                                    tag, t, cnt);
             mode = MODE_SHADE;
         }
         const uint64_t c1 = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
@@ -2618,7 +2649,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
         };
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
-            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, tboxes, P.num_prims, ro, rd, hit, tag, t, cnt);
+            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, tboxes, P.num_prims, P.flat_runs[0], P.flat_runs[1], ro, rd, hit, tag,
+                                    t, cnt);
             mode = MODE_SHADE;
         }
         pass_stamp(1);
@@ -3527,6 +3559,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.prims = (const float4*)S.prims_flat;
         P.ref_nodes = (const float4*)S.ref_nodes;
         P.flat_boxes = (const float4*)S.flat_boxes;
+        P.flat_runs[0] = S.flat_runs[0];
+        P.flat_runs[1] = S.flat_runs[1];
     }
     P.rius_cap = g_rius_trips > 0 ? (uint32_t)g_rius_trips : 0xffffffffu;  // (the flat kernels')
     const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave

@@ -74,6 +74,8 @@ struct HostScene {
     std::vector<float> ref_nodes;      // ... and the reference BVH itself: 8 floats per node (scene_build.cpp)
     std::vector<float> flat_boxes;     // ... and per flat record its reference box for the flat kernels' exactness
                                        // check: 8 floats (scene_build.cpp)
+    uint32_t flat_runs[2] = {0u, 0u};  // prims_flat holds each primitive type as one contiguous run: [begin, end) of
+                                        // type t in bytes 2t, 2t + 1 of the pair (t = RT_SPHERE .. RT_YZRECT)
     bool touching_rects = false;       // a rectangle's reference box touches or overlaps another primitive's: rays
                                        // there can tie or graze a box face (the automatic choice keeps such scenes
                                        // of <= kFlatMaxPrims primitives on the exact flat kernels)

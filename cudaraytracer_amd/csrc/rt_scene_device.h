@@ -18,6 +18,7 @@ struct DeviceScene {
     const void* ref_nodes = nullptr;   // the reference BVH (boxes + shape) over prims_flat, or NULL
     const void* flat_boxes = nullptr;  // per prims_flat record its reference box (exactness check), or NULL
     bool touching_rects = false;       // HostScene::touching_rects
+    uint32_t flat_runs[2] = {0u, 0u};  // HostScene::flat_runs
     const void* mats = nullptr;    // float4 × 3 per material
     const void* imgs = nullptr;    // int4 per image
     const void* texels = nullptr;  // RGB8

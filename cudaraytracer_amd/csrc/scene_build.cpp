@@ -597,6 +597,30 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
                 pack_prim(desc->hittables[ord[i]], out->prims_flat.data() + i * 8);
                 pack_flat_box(desc->hittables[ord[i]], out->flat_boxes.data() + i * 8);
             }
+            // the flat kernels scan one primitive type at a time (no per-primitive type branch): the reference test
+            // order keeps each type contiguous (the tree splits at type-group boundaries, BVHNode's type sort); a
+            // scene where it would not (never seen) simply does not get the flat kernels
+            uint32_t runs[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};
+            bool contiguous = true;
+            for (size_t i = 0; i < ord.size();) {
+                const int ty = desc->hittables[ord[i]].type;
+                size_t j = i;
+                while (j < ord.size() && desc->hittables[ord[j]].type == ty) j++;
+                if (runs[ty][1] != 0u) contiguous = false;  // a second run of the same type
+                runs[ty][0] = (uint32_t)i;
+                runs[ty][1] = (uint32_t)j;
+                i = j;
+            }
+            for (int ty = 0; ty < 4; ty++) {
+                const uint32_t v = runs[ty][0] | (runs[ty][1] << 8);
+                out->flat_runs[ty / 2] |= v << (16 * (ty % 2));
+            }
+            if (!contiguous) {
+                out->prims_flat.clear();
+                out->flat_boxes.clear();
+                out->flat_runs[0] = out->flat_runs[1] = 0u;
+                return RT_OK;
+            }
             // per node: (lo.xyz, child 0) (hi.xyz, child 1); a primitive child is ~(its flat index)
             out->ref_nodes.resize(rn.size() * 8);
             for (size_t i = 0; i < rn.size(); i++) {

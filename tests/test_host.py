@@ -222,3 +222,20 @@ def test_scheduling_knobs_defaults_and_ranges():
         for b in bad:
             assert abi.STATUS.get(L.rt_set_tuning(key, b)) == "RT_ERR_INVALID_ARGUMENT", (key, b)
         assert L.rt_set_tuning(key, default) == default  # unchanged by the refused values
+
+
+def test_queue_knobs_defaults_and_ranges():
+    """rt_set_tuning for the persistent kernels' queue (CPU: no kernel runs): chunk (multiple of 64), head stride
+    (power of two), chunk prefetch threshold (include/rt_hip.h RT_TUNE_QUEUE_PREFETCH)."""
+    L = lib()
+    for key, default, good, bad in [(abi.RT_TUNE_QUEUE_CHUNK, 64, 128, [0, 96, 4160]),
+                                    (abi.RT_TUNE_QUEUE_STRIDE, 128, 4096, [64, 192, 8192]),
+                                    (abi.RT_TUNE_QUEUE_PREFETCH, QUEUE_PREFETCH_DEFAULT, 48, [-1, 65])]:
+        prev = L.rt_set_tuning(key, good)
+        assert prev == default, (key, prev)
+        for b in bad:
+            assert abi.STATUS.get(L.rt_set_tuning(key, b)) == "RT_ERR_INVALID_ARGUMENT", (key, b)
+        assert L.rt_set_tuning(key, default) == good
+
+
+QUEUE_PREFETCH_DEFAULT = 0
