@@ -2288,6 +2288,19 @@ __device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, cons
 // a rectangle's t is NaN only as 0 · inf, so only on rays with a zero or infinite 1/d component or a non-finite
 // origin (geometry is finite, scene_build.cpp); a wave holding such a ray re-runs the rectangles' t for it after the
 // scan.  Those rays (about 1e-5 of them) replay the reference exactly (ref_trace); the rest are exact as they stand.
+// m's lane bit ? a : b, with the lane mask m read from SGPRs by the select itself (v_cndmask_b32 with an SGPR-pair
+// condition)
+__device__ __forceinline__ float select_m(const uint64_t m, const float a, const float b) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+__device__ __forceinline__ uint32_t select_m(const uint64_t m, const uint32_t a, const uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+
 template <bool COUNT_TESTS>
 __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, const float4* __restrict__ rnodes,
                                            const float4* __restrict__ boxes, const uint32_t n, const uint32_t runs0,
@@ -2317,13 +2330,14 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
         const float t = (q0.x - ok) * ik;
         const float xx = oa + t * da;
         const float yy = ob + t * db;
-        // (non-short-circuit & and |: lane-mask arithmetic, no branch)
-        const bool acc = (!(t < kTmin) & !(t > t_best)) & (!(xx < q0.y) & !(xx > q0.z) & !(yy < q0.w) & !(yy > q1.x));
-        const uint64_t acc_m = __ballot(acc);
+        // the acceptance as an SGPR lane mask: each comparison's ballot is one v_cmp into SGPRs, combined by SALU; the
+        // selects read the mask directly (a bool would be materialised as 0/1 and compared again, 8 issue cycles)
+        const uint64_t acc_m = __ballot(!(t < kTmin)) & __ballot(!(t > t_best)) & __ballot(!(xx < q0.y)) &
+                               __ballot(!(xx > q0.z)) & __ballot(!(yy < q0.w)) & __ballot(!(yy > q1.x));
         tie_m = (tie_m & ~acc_m) | (acc_m & __ballot(t == t_best));
-        t_best = acc ? t : t_best;
-        hit = acc ? (int)i : hit;
-        tag = acc ? __float_as_uint(q1.w) : tag;
+        t_best = select_m(acc_m, t, t_best);
+        hit = (int)select_m(acc_m, i, (uint32_t)hit);
+        tag = select_m(acc_m, __float_as_uint(q1.w), tag);
     };
     // wave-uniform record: scalar loads through the constant cache
     const auto record = [&](const uint32_t i, float4& q0, float4& q1) {
@@ -2356,13 +2370,15 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
             const float sq = sqrt_fast(real ? disc : 1.0f);  // (a dummy argument keeps sqrt_fast's fast path)
             const float tn = fast_div ? div_rn(-b - sq, a_dd, inv_a) : (-b - sq) / a_dd;
             const float tf = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
-            const bool near_ok = (tn < t_best) & (tn > kTmin);
-            const float t = near_ok ? tn : tf;  // the far root is tried only when the near one is out of range
-            const bool acc = real & (t < t_best) & (t > kTmin);
-            tie_m = (tie_m | __ballot(real & ((tn == t_best) | (!near_ok & (tf == t_best))))) & ~__ballot(acc);
-            t_best = acc ? t : t_best;
-            hit = acc ? (int)i : hit;
-            tag = acc ? __float_as_uint(q1.w) : tag;
+            // (lane masks in SGPRs, as the rectangles' acceptance below)
+            const uint64_t real_m = __ballot(real);
+            const uint64_t near_m = __ballot(tn < t_best) & __ballot(tn > kTmin);
+            const float t = select_m(near_m, tn, tf);  // the far root is tried only when the near one is out of range
+            const uint64_t acc_m = real_m & __ballot(t < t_best) & __ballot(t > kTmin);
+            tie_m = (tie_m | (real_m & (__ballot(tn == t_best) | (~near_m & __ballot(tf == t_best))))) & ~acc_m;
+            t_best = select_m(acc_m, t, t_best);
+            hit = (int)select_m(acc_m, i, (uint32_t)hit);
+            tag = select_m(acc_m, __float_as_uint(q1.w), tag);
         }
     }
     run(RT_XYRECT, rb, re);
