@@ -30,6 +30,8 @@ RT_TUNE_LDS_PAD, RT_TUNE_ADAPTIVE_ORDER, RT_TUNE_TEXEL_LAYOUT, RT_TUNE_QUEUE_CHU
 RT_TUNE_QUEUE_STRIDE, RT_TUNE_REGEN_LIVE_FRAC, RT_TUNE_LEAF_BREAK, RT_TUNE_RIUS_TRIPS = 8, 9, 10, 11
 RT_TUNE_FLAT_MAX = 12
 RT_TUNE_QUEUE_PREFETCH = 13
+RT_TUNE_QUEUE_GUIDE = 14
+RT_TUNE_QUEUE_MIN_CHUNK = 15
 
 STATUS = {
     0: "RT_OK",

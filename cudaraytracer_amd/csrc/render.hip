@@ -239,6 +239,7 @@ struct KParams {
     uint32_t work_total;       // v4: work indices in the frame (64 per 8×8 tile)
     uint32_t work_per_counter; // v4: indices per queue head (a multiple of 64): head k owns [k·n, (k+1)·n)
     uint32_t queue_prefetch;   // persistent kernels: fetch the next chunk once at most this many indices are left (0: off)
+    uint32_t queue_guide, queue_min;  // persistent kernels: guided chunk sizes (PixelQueue::chunk_want; 0: off)
     uint32_t lds_wave_words;   // v3/v4: LDS words per wave (parked state + stack)
     uint32_t rng_key_lo, rng_key_hi, rng_frame;  // RT_FLAG_RNG_PHILOX: Philox key (seed) and frame counter
     unsigned long long* wave_trace;  // diagnostic: v3 / flat per tile {start, end} of s_memrealtime (100 MHz); the
@@ -1964,7 +1965,16 @@ struct PixelQueue {
     bool pf_valid = false;                 // wave-uniform: an atomic on head qc is in flight for the next chunk
     uint32_t pf_base = 0u, pf_leader = 0u, pf_want = 0u;
     __device__ explicit PixelQueue(uint32_t head) : qc(head) {}
+    // Indices to take per atomic.  Guided (P.queue_guide > 0, RT_TUNE_QUEUE_GUIDE): the head's remaining indices over
+    // (waves per head × k), in multiples of 16 between P.queue_min and P.work_chunk — the private reserve of every
+    // wave shrinks as its head drains, so when the queue runs dry no wave still holds a full chunk that its lanes
+    // take out over a whole pixel lifetime before rendering it (C5's tail, profiles/r05b_c5_tail.txt).  Otherwise
+    // round 3's rule: P.work_chunk while the head had at least four chunks at this wave's last grab, then 64.
     __device__ __forceinline__ uint32_t chunk_want(const KParams& P) const {
+        if (P.queue_guide) {
+            const uint32_t g = (head_left / P.queue_guide) & ~15u;
+            return min(P.work_chunk, max(g, P.queue_min));
+        }
         return head_left > 4u * P.work_chunk ? P.work_chunk : 64u;
     }
     // Lanes with `need` take the next work indices of the wave's chunk (ballot + mbcnt rank); start(x, g, pix) runs on
@@ -3066,6 +3076,8 @@ constexpr uint32_t kQueueMaxStride = 4096;  // bytes between heads (RT_TUNE_QUEU
 thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's queue heads
 thread_local int g_queue_chunk = 64;    // RT_TUNE_QUEUE_CHUNK: work indices per queue atomic
 thread_local int g_queue_prefetch = 0;  // RT_TUNE_QUEUE_PREFETCH: fetch the next chunk ahead at this many indices left
+thread_local int g_queue_guide = 0;     // RT_TUNE_QUEUE_GUIDE: guided chunks, head_left / (waves per head × this)
+thread_local int g_queue_min = 16;      // RT_TUNE_QUEUE_MIN_CHUNK: the guided chunks' floor
 constexpr int kMaxDevices = 64;
 struct QueueRing {
     uint32_t* buf = nullptr;
@@ -3316,6 +3328,24 @@ int rt_set_tuning(int key, int value) {
         }
         int prev = g_flat_max;
         g_flat_max = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_GUIDE) {
+        if (value < 0 || value > 64) {
+            set_error("rt_set_tuning: queue guide factor must be in [0, 64]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_guide;
+        g_queue_guide = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_MIN_CHUNK) {
+        if (value < 16 || value > 64 || value % 16) {
+            set_error("rt_set_tuning: guided chunk floor must be 16, 32, 48 or 64");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_min;
+        g_queue_min = value;
         return prev;
     }
     if (key == RT_TUNE_QUEUE_PREFETCH) {
@@ -3596,6 +3626,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.pixel_cost = g_pixel_cost_bytes >= (uint64_t)P.work_total ? g_pixel_cost : nullptr;
         P.work_chunk = (uint32_t)g_queue_chunk;
         P.queue_prefetch = (uint32_t)g_queue_prefetch;
+        P.queue_min = (uint32_t)g_queue_min;
         P.queue_stride = (uint32_t)g_queue_stride / 4u;
         P.work_per_counter = (tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
         // the persistent flat kernel runs 4 waves per SIMD even where its registers allow 5-6: C5 0.294 vs 0.307 ms
@@ -3604,6 +3635,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
         grid = (uint32_t)(resident < grid ? resident : grid);
+        P.queue_guide = g_queue_guide > 0 ? std::max(1u, grid / dev::kQueueCounters) * (uint32_t)g_queue_guide : 0u;
         // (no reset here: the slot is zero, the previous launch that used it left it so, queue_release)
     }
     P.num_tiles = tiles;
