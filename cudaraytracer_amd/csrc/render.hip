@@ -3075,7 +3075,7 @@ constexpr uint32_t kQueueSlots = 256;
 constexpr uint32_t kQueueMaxStride = 4096;  // bytes between heads (RT_TUNE_QUEUE_STRIDE)
 thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's queue heads
 thread_local int g_queue_chunk = 64;    // RT_TUNE_QUEUE_CHUNK: work indices per queue atomic
-thread_local int g_queue_prefetch = 0;  // RT_TUNE_QUEUE_PREFETCH: fetch the next chunk ahead at this many indices left
+thread_local int g_queue_prefetch = 32; // RT_TUNE_QUEUE_PREFETCH: fetch the next chunk ahead at this many indices left
 thread_local int g_queue_guide = 0;     // RT_TUNE_QUEUE_GUIDE: guided chunks, head_left / (waves per head × this)
 thread_local int g_queue_min = 16;      // RT_TUNE_QUEUE_MIN_CHUNK: the guided chunks' floor
 constexpr int kMaxDevices = 64;

@@ -379,7 +379,8 @@ int rt_last_variant(void);
  *   Philox mode rounds it up to whole blocks of four attempts).  It does not change the image.
  *   RT_TUNE_QUEUE_PREFETCH: the persistent kernels (variants 4, 6) fetch their next chunk of work indices (the queue
  *   atomic) ahead, once at most this many indices of the current chunk are left, so the atomic's round trip overlaps
- *   the wave's work (0 = off: fetched when the chunk runs out; 0..64).  RT_TUNE_QUEUE_GUIDE: guided chunk sizes for
+ *   the wave's work (0 = off: fetched when the chunk runs out; 0..64; default 32: C5 -7 %,
+ *   profiles/r05g_ab_c5_queue_prefetch.txt).  RT_TUNE_QUEUE_GUIDE: guided chunk sizes for
  *   the persistent kernels — a wave takes (its head's remaining indices) / (waves per head × this factor), rounded
  *   down to a multiple of 16, at least RT_TUNE_QUEUE_MIN_CHUNK (16..64) and at most RT_TUNE_QUEUE_CHUNK (0 = off:
  *   RT_TUNE_QUEUE_CHUNK while plenty is left, then 64; 0..64).  None of these changes the image. */

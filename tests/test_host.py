@@ -230,7 +230,9 @@ def test_queue_knobs_defaults_and_ranges():
     L = lib()
     for key, default, good, bad in [(abi.RT_TUNE_QUEUE_CHUNK, 64, 128, [0, 96, 4160]),
                                     (abi.RT_TUNE_QUEUE_STRIDE, 128, 4096, [64, 192, 8192]),
-                                    (abi.RT_TUNE_QUEUE_PREFETCH, QUEUE_PREFETCH_DEFAULT, 48, [-1, 65])]:
+                                    (abi.RT_TUNE_QUEUE_PREFETCH, QUEUE_PREFETCH_DEFAULT, 48, [-1, 65]),
+                                    (abi.RT_TUNE_QUEUE_GUIDE, QUEUE_GUIDE_DEFAULT, 4, [-1, 65]),
+                                    (abi.RT_TUNE_QUEUE_MIN_CHUNK, 16, 32, [0, 24, 80])]:
         prev = L.rt_set_tuning(key, good)
         assert prev == default, (key, prev)
         for b in bad:
@@ -238,4 +240,5 @@ def test_queue_knobs_defaults_and_ranges():
         assert L.rt_set_tuning(key, default) == good
 
 
-QUEUE_PREFETCH_DEFAULT = 0
+QUEUE_PREFETCH_DEFAULT = 32
+QUEUE_GUIDE_DEFAULT = 0
