@@ -640,14 +640,22 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, con
         ro = p;
         return SHADE_CONTINUE;
     }
+    // The attenuation (texture lookup) before the rejection loop, which it does not depend on: an image texel's gather
+    // is in flight while RandomInUnitSphere runs instead of after it (no RNG draw moves)
+    const float4 m1 = mats[3 * mat + 1];
+    f3 attenuation;
+    if (!TEX || ttype == RT_CONSTANT) {
+        attenuation = xyz(m1);
+    } else {
+        const float4 m2 = mats[3 * mat + 2];
+        attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, imgs, P->texels);
+    }
     f3 q;
     if constexpr (DEFER) {
         if (!random_in_unit_sphere_capped(rng, rtl, P->rius_cap, q)) return SHADE_DEFERRED;
     } else {
         q = random_in_unit_sphere(rng, rtl);
     }
-    const float4 m1 = mats[3 * mat + 1];
-    f3 attenuation;
     bool ok = true;
     if (mtype == RT_LAMBERTIAN) {  // Lambertian::Scatter (Material.cuh:43-62)
         const f3 target = add(add(p, normal), q);
@@ -656,12 +664,6 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, con
         const f3 reflected = reflect(ud, normal);
         rd = add(reflected, scale(m0.y, q));
         ok = dot(rd, normal) > 0;
-    }
-    if (!TEX || ttype == RT_CONSTANT) {
-        attenuation = xyz(m1);
-    } else {
-        const float4 m2 = mats[3 * mat + 2];
-        attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, imgs, P->texels);
     }
     ro = p;
     if (ok) {
