@@ -251,7 +251,7 @@ enum rt_render_flags {
                                       (each sample's window is 2^18 words; larger spp is rejected); a sample's
                                       channel below 2^-13 (and any negative or NaN value) rounds to 0, so a
                                       very dim image loses up to 2^-13 per sample and channel against the
-                                      parity mode's float sum (tests/test_gpu_parity.py dim-scene check). */
+                                      parity mode's float sum (tests/test_oracle.py::test_philox_mode_dim_scene_bias_is_bounded). */
     RT_FLAG_ACCUMULATE_RESET = 1u << 7, /* with RT_FLAG_ACCUMULATE: the accumulation restarts with this frame
                                             (a camera move or scene edit): accum is written, never read — the
                                             same bits as zeroing it first (0 + x rounds as the kernel adds),

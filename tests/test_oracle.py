@@ -428,3 +428,30 @@ def test_flop_model_prices_rectangle_and_sphere_tests_apart():
     _, _, ref = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, inp, st)
     assert [ref.rays, ref.box_tests, ref.prim_tests, ref.primary] == [int(x) for x in load_golden(case.name)["counters"]]
     assert 0 < ref.rect_tests < ref.prim_tests
+
+
+def test_philox_mode_dim_scene_bias_is_bounded():
+    """The Philox mode sums each sample's channel rounded to the nearest multiple of 2^-12 (include/rt_hip.h
+    RT_FLAG_RNG_PHILOX; quant12 in render.hip, orc_quant here), so a sample contributes its value within 2^-13, and a
+    positive value below 2^-13 contributes 0.  In a dim scene (RTIOW under a sky 1/256 as bright: most samples carry
+    a few 2^-12 or less) the per-channel image mean of (philox - xorwow) pre-gamma radiance stays within 4 standard
+    errors plus the rounding's 2^-13 bound (the low-end energy the fixed point loses is bounded and tested)."""
+    cfg = scenes.CONFIGS["c2"].scaled(96, 54, 32)
+    inp = cfg.inputs()
+    for i in range(3):
+        inp.background_start[i] = inp.background_start[i] / 256.0
+        inp.background_end[i] = inp.background_end[i] / 256.0
+    sc = po.OracleScene(scenes.builtin(cfg.scene))
+    _, rx, _ = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, inp, po.init_states(cfg.width, cfg.height),
+                         radiance=True, threads=8)
+    _, rp, _ = po.render(sc, cfg.width, cfg.height, cfg.spp, cfg.depth, inp, None, radiance=True, philox=True,
+                         threads=8)
+    x = rx[..., :3].astype(np.float64).reshape(-1, 3)
+    p = rp[..., :3].astype(np.float64).reshape(-1, 3)
+    assert 0.0 < x.mean() < 8.0 / 4096  # dim: the mean sample is a few quanta (measured 4.5)
+    d = p - x
+    se = d.std(axis=0) / math.sqrt(d.shape[0])
+    assert np.all(np.abs(d.mean(axis=0)) < 4 * se + 2.0 ** -13), (d.mean(axis=0), se)
+    # every Philox pixel mean is a whole number of quanta over spp (the fixed-point sum), XORWOW's is not
+    q = p * 4096.0 * cfg.spp
+    assert np.allclose(q, np.round(q), atol=1e-3 * cfg.spp)
