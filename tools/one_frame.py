@@ -23,7 +23,12 @@ ds = DeviceScene(cfg.scene_desc())  # c5: three 8192x4096 textures
 r = Renderer(cfg.width, cfg.height, rng=args.rng, state_layout=args.state_layout)
 r.render_init()
 flags = abi.RT_FLAG_ACCUMULATE if args.config == "c5" else 0
-for _ in range(args.frames):
-    r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=flags)
+for f in range(args.frames):
+    inp = cfg.inputs()
+    if args.config == "c5":  # as bench.py renders C5: the scripted orbit, the accumulation restarted per frame
+        pos, fwd = scenes.moving_camera(f, 60)
+        inp = scenes.camera_inputs(pos, fwd, cfg.fov)
+        r.reset_accumulation()
+    r.render(ds, cfg.spp, cfg.depth, inp, flags=flags)
 torch.cuda.synchronize()
 print("rays/frame", int(r.counters[0]) // args.frames)

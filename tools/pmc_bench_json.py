@@ -21,7 +21,7 @@ if len(sys.argv) > 2 and sys.argv[1] == "--config":
     CONFIG = sys.argv[2]
     del sys.argv[1:3]
 PIXELS = {"c2": 1920 * 1080, "c3": 3840 * 2160, "c5": 1920 * 1080}[CONFIG]
-ACCUM = 32 if CONFIG == "c5" else 0
+ACCUM = 16 if CONFIG == "c5" else 0  # c5: each frame restarts the accumulation (camera moves): float4 written, not read
 
 
 def passes(out):
