@@ -485,8 +485,10 @@ def valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world) -> dict:
     achieved = f_launch / (kernel_ms * 1e-3) / 1e12
     # HBM bytes per launch: the committed N=1 PMC summary of this config.  A rank's bytes do not depend on spp
     # (per pixel: RNG state in and out, one RGBA8 store), so other frame shapes scale it by the rank's pixels.
-    pmc = pmc_profile(args.config if args.config != "c4" else "c2", args.rng, args.state_layout)
-    base = scenes.CONFIGS[args.config if args.config != "c4" else "c2"]
+    # (config 4: its own PMC summary when committed, else C2's per-pixel bytes scaled)
+    pmc_cfg = args.config if args.config != "c4" or pmc_profile("c4", args.rng, args.state_layout) else "c2"
+    pmc = pmc_profile(pmc_cfg, args.rng, args.state_layout)
+    base = scenes.CONFIGS[pmc_cfg]
     pix_scale = r.local_rows * cfg.width / (base.width * base.height)
     if "hbm_bytes_per_launch" in pmc and pix_scale != 1.0:
         for k in ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch"):
@@ -503,7 +505,7 @@ def valu_roofline(args, cfg, r, c, f_launch, kernel_ms, world) -> dict:
         "scope": ("per rank: rank 0's counted FLOP per launch / the slowest rank's kernel time, against one GPU's "
                   "peak" if world > 1 else "one launch = one frame"),
         "traffic": pmc.get("hbm_bytes_per_launch"),
-        "traffic_source": ((f"rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_{args.config if args.config != 'c4' else 'c2'}_n1.json"
+        "traffic_source": ((f"rocprofv3 PMC FETCH_SIZE*2 + WRITE_SIZE, profiles/pmc_{pmc_cfg}_n1.json"
                             + (" (per-pixel bytes x this rank's pixels)" if pmc.get("scaled") else ""))
                            if "hbm_bytes_per_launch" in pmc else None),
         "algorithmic_hbm_bytes": pmc.get("algorithmic_bytes_per_launch"),

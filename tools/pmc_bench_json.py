@@ -20,7 +20,7 @@ CONFIG = "c2"
 if len(sys.argv) > 2 and sys.argv[1] == "--config":
     CONFIG = sys.argv[2]
     del sys.argv[1:3]
-PIXELS = {"c2": 1920 * 1080, "c3": 3840 * 2160, "c5": 1920 * 1080}[CONFIG]
+PIXELS = {"c2": 1920 * 1080, "c3": 3840 * 2160, "c4": 7680 * 4320, "c5": 1920 * 1080}[CONFIG]
 ACCUM = 16 if CONFIG == "c5" else 0  # c5: each frame restarts the accumulation (camera moves): float4 written, not read
 
 
