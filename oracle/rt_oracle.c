@@ -506,8 +506,39 @@ int orc_scene_depth(const orc_scene* s) { return s->depth; }
  * orc_scene_depth(). */
 typedef struct { int node; float tmin, tmax; } stacknode;
 
+#ifdef ORC_HIT_DIAG
+/* Diagnostic build only (tools/bvh_hit_class.py compiles it with -DORC_HIT_DIAG into /tmp; the library the tests load
+ * never has it): every reference-BVH closest-hit query is repeated as the exact linear scan and a disagreement is
+ * classed as [1] tie (same t, another primitive's material/normal) or [2] culled (the BVH answer is farther or a miss:
+ * a box rejected the ray at the precision edge of its slab test) or [3] other; [0] counts all disagreements. */
+static unsigned long long orc_diag_counts[4];
+unsigned long long orc_hit_diag(int k) { return k >= 0 && k < 4 ? orc_diag_counts[k] : 0; }
+static int world_hit_bvh(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, hitrec* rec,
+                         unsigned long long* box_tests, unsigned long long* prim_tests, unsigned long long* rect_tests);
 static int world_hit(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, hitrec* rec,
                      unsigned long long* box_tests, unsigned long long* prim_tests, unsigned long long* rect_tests) {
+    int r = world_hit_bvh(s, o, d, tmin, tmax, rec, box_tests, prim_tests, rect_tests);
+    if (s->exact_closest_hit) return r;
+    hitrec e;
+    int he = 0;
+    for (int i = 0; i < s->nprims; i++)
+        if (s->prims[i].is_active) he |= prim_hit(&s->prims[i], o, d, tmin, he ? e.t : tmax, &e);
+    if (he == r && (!he || (e.t == rec->t && e.mat == rec->mat && e.normal.x == rec->normal.x &&
+                            e.normal.y == rec->normal.y && e.normal.z == rec->normal.z)))
+        return r;
+    int k = (he && r && e.t == rec->t) ? 1 : (he && (!r || rec->t > e.t)) ? 2 : 3;
+#pragma omp atomic
+    orc_diag_counts[0]++;
+#pragma omp atomic
+    orc_diag_counts[k]++;
+    return r;
+}
+static int world_hit_bvh(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, hitrec* rec,
+                         unsigned long long* box_tests, unsigned long long* prim_tests, unsigned long long* rect_tests) {
+#else
+static int world_hit(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, hitrec* rec,
+                     unsigned long long* box_tests, unsigned long long* prim_tests, unsigned long long* rect_tests) {
+#endif
     if (s->exact_closest_hit) {
         /* Geometric closest hit over the active primitives in list order, without box culling. */
         int hit_something = 0;
