@@ -80,20 +80,46 @@ def procedural_texture(kind: int = TEXTURE_EARTH, width: int = 1024, height: int
     return img
 
 
-def builtin(which: int, seed: int = 1, texture_size: tuple = DEFAULT_TEXTURE_SIZE) -> Scene:
+def load_image(filename: str) -> np.ndarray | None:
+    """The reference's LoadImage (Utils/RawStbImage.h:11-22, stbi_load with desired_channels 0): the decoded file as
+    (height, width, channels) uint8, row 0 at the top, channels as stored (3 for the reference's 8K planet maps, which
+    is what Image::value reads, Texture.cuh:76), or None when the file cannot be decoded — the reference logs the
+    error and hands back a null pointer (CudaLayer.cpp:895).  Decoding is host work and uses Pillow; Pillow's
+    libjpeg and stb's decoder may round some texels differently (parity unpinned against stb)."""
+    try:
+        from PIL import Image as _PIL
+    except ImportError as e:  # pragma: no cover - Pillow is part of this image
+        raise RuntimeError("load_image needs Pillow to decode image files") from e
+    try:
+        with _PIL.open(filename) as im:
+            im.load()
+            if im.mode not in ("L", "LA", "RGB", "RGBA"):
+                im = im.convert("RGBA" if "A" in im.getbands() else "RGB")
+            a = np.asarray(im, dtype=np.uint8)
+    except (OSError, ValueError):
+        return None
+    return np.ascontiguousarray(a if a.ndim == 3 else a[:, :, None])
+
+
+def builtin(which: int, seed: int = 1, texture_size: tuple = DEFAULT_TEXTURE_SIZE, images: list | None = None) -> Scene:
     """Built-in scene `which` (see rt_builtin_scene in include/rt_hip.h).  The textured scene gets three
-    procedural images (earth, moon, sun) of texture_size = (width, height)."""
+    procedural images (earth, moon, sun) of texture_size = (width, height), or the caller's `images` — RGB8
+    (H, W, 3) arrays, e.g. from load_image on the reference's assets/textures files."""
     L = lib()
     nh, nm = C.c_uint32(0), C.c_uint32(0)
     check(L.rt_builtin_scene(which, seed, None, C.byref(nh), None, C.byref(nm)), "rt_builtin_scene(size)")
     h = (abi.HittableDesc * nh.value)()
     m = (abi.MaterialDesc * nm.value)()
     check(L.rt_builtin_scene(which, seed, h, C.byref(nh), m, C.byref(nm)), "rt_builtin_scene")
-    images = []
-    if which == SCENE_TEXTURED:
+    imgs = []
+    if which == SCENE_TEXTURED and images is not None:
+        if len(images) != 3 or any(im.ndim != 3 or im.shape[2] != 3 or im.dtype != np.uint8 for im in images):
+            raise ValueError("the textured scene takes three RGB8 (H, W, 3) uint8 images (earth, moon, sun)")
+        imgs = [np.ascontiguousarray(im) for im in images]
+    elif which == SCENE_TEXTURED:
         w, hh = texture_size
-        images = [procedural_texture(k, w, hh) for k in (TEXTURE_EARTH, TEXTURE_MOON, TEXTURE_SUN)]
-    return Scene(h, m, images)
+        imgs = [procedural_texture(k, w, hh) for k in (TEXTURE_EARTH, TEXTURE_MOON, TEXTURE_SUN)]
+    return Scene(h, m, imgs)
 
 
 def camera_inputs(position, orientation, fov_degrees, near=0.1, far=10.0, world_up=(0.0, 1.0, 0.0),

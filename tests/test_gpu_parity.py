@@ -946,3 +946,4 @@ def test_trace_rays_matches_brute_force_closest_hit():
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
         assert int(cnt[0]) == n and int(cnt[1]) > 2 * n
     assert np.isfinite(best).mean() > 0.3
+

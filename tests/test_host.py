@@ -3,6 +3,7 @@ validation, the BVH build and the reference-graph flattener (no device needed)."
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -242,3 +243,46 @@ def test_queue_knobs_defaults_and_ranges():
 
 QUEUE_PREFETCH_DEFAULT = 32
 QUEUE_GUIDE_DEFAULT = 0
+
+
+# ---------------------------------------------------------------------------------------------------
+# Image loading (LoadImage, Utils/RawStbImage.h:11-22) and the reference's own texture assets
+# ---------------------------------------------------------------------------------------------------
+REF_TEXTURES = "/root/reference/assets/textures"
+
+
+def test_load_image_mirrors_loadimage(tmp_path):
+    from PIL import Image
+
+    rgb = (np.arange(5 * 7 * 3, dtype=np.uint8) * 7).reshape(5, 7, 3)
+    Image.fromarray(rgb).save(tmp_path / "a.png")
+    got = scenes.load_image(str(tmp_path / "a.png"))
+    assert got.shape == (5, 7, 3) and np.array_equal(got, rgb)  # row 0 at the top, as stb decodes
+    grey = rgb[:, :, 0]
+    Image.fromarray(grey).save(tmp_path / "g.png")
+    assert scenes.load_image(str(tmp_path / "g.png")).shape == (5, 7, 1)  # channels as stored (desired_channels 0)
+    assert scenes.load_image(str(tmp_path / "missing.jpg")) is None  # the reference logs and returns nullptr
+    (tmp_path / "bad.jpg").write_bytes(b"not a jpeg")
+    assert scenes.load_image(str(tmp_path / "bad.jpg")) is None
+
+
+def test_textured_scene_takes_caller_images():
+    imgs = [np.full((64, 128, 3), v, dtype=np.uint8) for v in (10, 20, 30)]
+    sc = scenes.builtin(scenes.SCENE_TEXTURED, images=imgs)
+    assert [im.shape for im in sc.images] == [(64, 128, 3)] * 3
+    with pytest.raises(ValueError):
+        scenes.builtin(scenes.SCENE_TEXTURED, images=imgs[:2])
+    with pytest.raises(ValueError):
+        scenes.builtin(scenes.SCENE_TEXTURED, images=[imgs[0], imgs[1], imgs[2][:, :, :1]])
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_TEXTURES), reason="the reference's assets are not here")
+def test_reference_texture_files_load_as_rgb8():
+    """The reference's own planet maps, read in place (nothing derived from them is stored): each decodes to the
+    RGB8 layout Image::value reads (Texture.cuh:76) and sits on the textured scene's spheres."""
+    imgs = [scenes.load_image(os.path.join(REF_TEXTURES, n)) for n in ("8k_earth_nightmap.jpg", "8k_stars.jpg",
+                                                                        "8k_sun.jpg")]
+    assert [im.shape for im in imgs] == [(4096, 8192, 3), (4096, 8192, 3), (2048, 4096, 3)]
+    sc = scenes.builtin(scenes.SCENE_TEXTURED, images=imgs)
+    d = sc.desc()
+    assert d.num_images == 3 and (d.images[2].width, d.images[2].height) == (4096, 2048)
