@@ -1951,6 +1951,10 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
 // atomic each and moves on to the next live head when its own is exhausted.  Chunks are P.work_chunk indices while
 // the head had plenty left at this wave's last grab, then 64 (other waves draining the same head make that count
 // stale, so a chunk above 64 can still lengthen the frame's tail: RT_TUNE_QUEUE_CHUNK defaults to 64).
+// TRACE: the wave-trace build (a persistent kernel's instance picked only while rt_set_wave_trace holds a buffer); the
+// product instances carry none of the trace's stamps and counters, whose SGPRs spilled to VGPR lanes (C5 kernel: 105
+// spilled SGPRs with them, 53 without; -2.5 % per frame, profiles/r05q_ab_c5_trace_build.txt).
+template <bool TRACE>
 struct PixelQueue {
     uint32_t qc;                           // the head the wave draws from
     uint32_t qtried = 0u;                  // heads found exhausted
@@ -1988,7 +1992,7 @@ struct PixelQueue {
             if (wq_next >= wq_end) {
                 uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
                 uint32_t base = 0u, want;
-                const uint64_t ta = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+                const uint64_t ta = TRACE ? __builtin_amdgcn_s_memrealtime() : 0u;
                 if (pf_valid) {  // the chunk fetched ahead (same head: qc changes only below, after consuming it)
                     leader = pf_leader;
                     want = pf_want;
@@ -2000,25 +2004,25 @@ struct PixelQueue {
                     base = __builtin_amdgcn_readlane(base, leader);
                 }
                 const uint32_t idx = qc * P.work_per_counter + base;
-                if (P.wave_trace) {  // (diagnostic: the atomic's round trip, stamped after its result is in)
+                if (TRACE) {  // (diagnostic: the atomic's round trip, stamped after its result is in)
                     __builtin_amdgcn_s_waitcnt(0);
                     rt_atomic += __builtin_amdgcn_s_memrealtime() - ta;
                 }
                 if (base >= P.work_per_counter || idx >= P.work_total) {  // this head is exhausted
                     // mark it in the exhausted-heads word and move to the next live head (so a wave probes a few
                     // heads at the frame's end, not every one of them)
-                    const uint64_t tb = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+                    const uint64_t tb = TRACE ? __builtin_amdgcn_s_memrealtime() : 0u;
                     uint32_t done = 0u;
                     if (__lane_id() == leader) done = atomicOr(P.work_counter + kQueueCounters * P.queue_stride, 1u << qc);
                     done = __builtin_amdgcn_readlane(done, leader) | (1u << qc);
-                    if (P.wave_trace) {
+                    if (TRACE) {
                         __builtin_amdgcn_s_waitcnt(0);
                         rt_atomic += __builtin_amdgcn_s_memrealtime() - tb;
                         n_probe++;
                     }
                     if (done == kQueueAllDone || ++qtried >= kQueueCounters) {
                         drained = true;
-                        if (P.wave_trace) rt_drained = __builtin_amdgcn_s_memrealtime();
+                        if (TRACE) rt_drained = __builtin_amdgcn_s_memrealtime();
                         break;
                     }
                     const uint32_t live = ~done & kQueueAllDone;        // (nonzero here)
@@ -2028,7 +2032,7 @@ struct PixelQueue {
                     continue;
                 }
                 wq_next = idx;
-                if (P.wave_trace) n_grab++;
+                if (TRACE) n_grab++;
                 // (a chunk ends at its head's range: a head's range is a multiple of 64, not of work_chunk)
                 wq_end = idx + min(want, P.work_per_counter - base);
                 head_left = P.work_per_counter - base - min(want, P.work_per_counter - base);
@@ -2045,7 +2049,7 @@ struct PixelQueue {
             }
             const uint32_t taken = min((uint32_t)__popcll(needm), avail);
             wq_next += taken;
-            if (P.wave_trace && taken) rt_last = __builtin_amdgcn_s_memrealtime();
+            if (TRACE && taken) rt_last = __builtin_amdgcn_s_memrealtime();
             const uint64_t still = __ballot(need);
             wave_pixels += (uint32_t)__popcll(needm & ~still);
             needm = still;
@@ -2079,8 +2083,9 @@ __device__ __forceinline__ void queue_release(const KParams& P) {
 // SIMD / CU / shader engine and XCD), [5] when it last handed out a pixel, [6] chunk grabs | exhausted-head probes
 // << 32, [7] realtime ticks spent waiting for the queue's atomics.  Times: s_memrealtime (100 MHz).
 constexpr uint32_t kWaveTraceWords = 8;
-__device__ __forceinline__ void trace_persistent_wave(const KParams& P, const PixelQueue& queue, uint64_t rt_start) {
-    if (P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (blockIdx.x + 1ull) <= P.wave_trace_words) {
+template <bool TRACE>
+__device__ __forceinline__ void trace_persistent_wave(const KParams& P, const PixelQueue<TRACE>& queue, uint64_t rt_start) {
+    if (TRACE && P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (blockIdx.x + 1ull) <= P.wave_trace_words) {
         unsigned long long* w = P.wave_trace + (size_t)kWaveTraceWords * blockIdx.x;
         w[0] = rt_start;
         w[1] = queue.rt_drained;
@@ -2094,7 +2099,8 @@ __device__ __forceinline__ void trace_persistent_wave(const KParams& P, const Pi
     }
 }
 
-template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false, int WAVES_PER_SIMD = 1>
+template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false, int WAVES_PER_SIMD = 1,
+          bool TRACE = false>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     using Entry = typename RefW<WIDE>::Entry;
@@ -2115,9 +2121,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
     f3 ro = mk(0.0f, 0.0f, 0.0f), rd = ro;
     Cursor c{(int)RefW<WIDE>::kSentinel, 0, -1, 0u, 0u, FLT_MAX, MODE_NEED};
-    PixelQueue queue(blockIdx.x % kQueueCounters);
+    PixelQueue<TRACE> queue(blockIdx.x % kQueueCounters);
     const uint32_t threshold = P.regen_threshold;
-    const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+    const uint64_t rt_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0u;
 
     while (true) {
         if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt);
@@ -2611,7 +2617,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
 // 168 -> 211 us; profiles/r04e_ab_c5_prefetch.txt).
 constexpr int kFlatPrefetch = 1;
 constexpr uint32_t kPrefetchStop = 8;
-template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD>
+template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD, bool TRACE = false>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persistent(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     constexpr bool kNext = (kFlatPrefetch & 1) && !PHILOX;  // (Philox has no per-pixel state to load)
@@ -2651,13 +2657,13 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     int hit = -1;
     uint32_t tag = 0u;
     float t = FLT_MAX;
-    PixelQueue queue(blockIdx.x % kQueueCounters);
-    const uint64_t rt_start = P.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0u;
+    PixelQueue<TRACE> queue(blockIdx.x % kQueueCounters);
+    const uint64_t rt_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0u;
     // pass trace (diagnostic, tools/c5_tail.py): every 64th wave stamps each of its first kPassTrace / 4 passes with 4
     // words: s_memrealtime at the pass start (bits 0-39) with the lanes about to trace (40-46), shade (47-53) and with a
     // pixel at all (54-60); then s_memrealtime after the trace, after the shading and after the queue
     constexpr uint32_t kPassTrace = 1024;
-    const bool pass_traced = P.wave_trace && (blockIdx.x & 63u) == 0u &&
+    const bool pass_traced = TRACE && P.wave_trace && (blockIdx.x & 63u) == 0u &&
                              (uint64_t)P.wave_trace_words >= (uint64_t)kWaveTraceWords * gridDim.x +
                                  (uint64_t)kPassTrace * (blockIdx.x / 64u + 1u);
     unsigned long long* const pass_rec =
@@ -2677,8 +2683,11 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
         };
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
-            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, tboxes, P.num_prims, P.flat_runs[0], P.flat_runs[1], ro, rd, hit, tag,
-                                    t, cnt);
+            // the scan's launch-uniform operands re-read per pass (s_load): hoisted out of the loop, the per-run
+            // pointers, counts and masks derived from them overflowed the SGPR budget into VGPR-lane spills
+            KParamsC* const q = kparams_reload();
+            flat_trace<COUNT_TESTS>(q->prims, q->ref_nodes, tboxes, q->num_prims, q->flat_runs[0], q->flat_runs[1], ro, rd,
+                                    hit, tag, t, cnt);
             mode = MODE_SHADE;
         }
         pass_stamp(1);
@@ -2902,12 +2911,16 @@ KernelFn v3_pick(bool count, bool tex) {
 // config-5 frame is not occupancy-bound: held to 5 / 6 / 8 waves it runs 0.30 / 0.33 / 0.51 ms against 0.293
 // (profiles/r03g_ab_v4_tex_waves.txt; 6 and 8 spill to scratch)
 constexpr int kV4TexWaves = 1;
+// trace: the wave-trace build of a persistent kernel (rt_set_wave_trace holds a buffer; counting builds carry no trace)
 template <bool PH = false, bool WD = false>
-KernelFn v4_pick(bool count, bool tex) {
+KernelFn v4_pick(bool count, bool tex, bool trace) {
     if (tex)
-        return count ? dev::render_kernel_v4<true, true, dev::NODES_64, PH, WD>
-                     : dev::render_kernel_v4<false, true, dev::NODES_64, PH, WD, kV4TexWaves>;
-    return count ? dev::render_kernel_v4<true, false, dev::NODES_64, PH, WD> : dev::render_kernel_v4<false, false, dev::NODES_64, PH, WD>;
+        return count   ? dev::render_kernel_v4<true, true, dev::NODES_64, PH, WD>
+               : trace ? dev::render_kernel_v4<false, true, dev::NODES_64, PH, WD, kV4TexWaves, true>
+                       : dev::render_kernel_v4<false, true, dev::NODES_64, PH, WD, kV4TexWaves>;
+    return count   ? dev::render_kernel_v4<true, false, dev::NODES_64, PH, WD>
+           : trace ? dev::render_kernel_v4<false, false, dev::NODES_64, PH, WD, 1, true>
+                   : dev::render_kernel_v4<false, false, dev::NODES_64, PH, WD>;
 }
 
 constexpr int kXorwowCompactWaves = 8;  // __launch_bounds__ waves per SIMD of the XORWOW build of variant 3
@@ -2916,24 +2929,28 @@ constexpr int kPhiloxCompactWaves = 8;  // ... of the non-texture Philox build o
 constexpr int kFlatWaves = 8;  // __launch_bounds__ waves per SIMD of the untextured flat kernel
 constexpr int kFlatPersistentWaves = 4;  // resident waves per SIMD of the persistent flat kernel's grid
 template <bool PH>
-KernelFn flat_pick(bool count, bool tex, bool persistent) {
+KernelFn flat_pick(bool count, bool tex, bool persistent, bool trace) {
     if (persistent) {
         if (tex)
-            return count ? dev::render_kernel_flat_persistent<true, true, PH, 1> : dev::render_kernel_flat_persistent<false, true, PH, 1>;
-        return count ? dev::render_kernel_flat_persistent<true, false, PH, 1> : dev::render_kernel_flat_persistent<false, false, PH, 1>;
+            return count   ? dev::render_kernel_flat_persistent<true, true, PH, 1>
+                   : trace ? dev::render_kernel_flat_persistent<false, true, PH, 1, true>
+                           : dev::render_kernel_flat_persistent<false, true, PH, 1>;
+        return count   ? dev::render_kernel_flat_persistent<true, false, PH, 1>
+               : trace ? dev::render_kernel_flat_persistent<false, false, PH, 1, true>
+                       : dev::render_kernel_flat_persistent<false, false, PH, 1>;
     }
     if (tex) return count ? dev::render_kernel_flat<true, true, PH, 1> : dev::render_kernel_flat<false, true, PH, 1>;
     return count ? dev::render_kernel_flat<true, false, PH, 1> : dev::render_kernel_flat<false, false, PH, kFlatWaves>;
 }
 
-KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
+KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide, bool trace) {
     if (variant == kVarFlat || variant == kVarFlatPersistent)
-        return philox ? flat_pick<true>(count, tex, variant == kVarFlatPersistent)
-                      : flat_pick<false>(count, tex, variant == kVarFlatPersistent);
+        return philox ? flat_pick<true>(count, tex, variant == kVarFlatPersistent, trace)
+                      : flat_pick<false>(count, tex, variant == kVarFlatPersistent, trace);
     if (wide) {  // 32-bit references: builds of the compact v3 and of v4 only (rt_render maps wide scenes there)
         if (variant == kVarV3Compact)
             return philox ? v3_pick<1, true, true, true>(count, tex) : v3_pick<1, false, true, true>(count, tex);
-        return philox ? v4_pick<true, true>(count, tex) : v4_pick<false, true>(count, tex);
+        return philox ? v4_pick<true, true>(count, tex, trace) : v4_pick<false, true>(count, tex, trace);
     }
     switch (variant) {
     case kVarV1: return count ? dev::render_kernel<true> : dev::render_kernel<false>;
@@ -2947,7 +2964,7 @@ KernelFn pick(int variant, bool count, bool tex, bool philox, bool wide) {
         if (philox)
             return tex ? v3_pick<1, true, true>(count, true) : v3_pick<kPhiloxCompactWaves, true, true>(count, false);
         return tex ? v3_pick<1, false, true>(count, true) : v3_pick<kXorwowCompactWaves, false, true>(count, false);
-    default: return philox ? v4_pick<true>(count, tex) : v4_pick<false>(count, tex);
+    default: return philox ? v4_pick<true>(count, tex, trace) : v4_pick<false>(count, tex, trace);
     }
 }
 
@@ -3602,7 +3619,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
     }
-    KernelFn fn = pick(variant, count_tests, S.has_textures, philox, wide);
+    KernelFn fn = pick(variant, count_tests, S.has_textures, philox, wide, g_wave_trace != nullptr);
     if (V.kernel == 5 || V.kernel == 6) {  // the flat kernels' tables: primitives in the reference's test order, its BVH
         P.prims = (const float4*)S.prims_flat;
         P.ref_nodes = (const float4*)S.ref_nodes;
