@@ -26,7 +26,8 @@ for step in $STEPS; do
         python3 bench.py --no-cpu-baseline --no-config-lines ${BENCH_ARGS:-} > gpurun_out/bench_prof.log 2>&1 || exit $? ;;
     benchcfg)  # driver-shaped lines for BASELINE configs 3 and 5
       for cfg in c5 c3; do
-        timeout -k 10 400 python bench.py --config $cfg --steps ${CFG_STEPS:-5} --warmup 2 ${BENCH_ARGS:-} \
+        steps=${CFG_STEPS:-5}; [ $cfg = c5 ] && steps=${C5_STEPS:-20}  # C5's orbit: average 20 frames, as other_configs.c5
+        timeout -k 10 400 python bench.py --config $cfg --steps $steps --warmup 2 ${BENCH_ARGS:-} \
           > gpurun_out/bench_$cfg.log 2>&1 || exit $?
         tail -1 gpurun_out/bench_$cfg.log
       done ;;
