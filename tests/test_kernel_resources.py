@@ -20,14 +20,15 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 # render_kernel_v3<COUNT_TESTS=false, W, TEX, PHILOX, COMPACT, WIDE> (variants 2 and 3; the untextured compact
 # 16-bit-reference builds are held to 8 waves per SIMD by registers (both RNG modes), render.hip
 # k*CompactWaves; the 32-bit-reference (WIDE) builds exist for the compact v3 and v4 only)
-# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX, WIDE, WAVES_PER_SIMD=1> (variant 4)
+# render_kernel_v4<COUNT_TESTS=false, TEX, NODES_64=2, PHILOX, WIDE, WAVES_PER_SIMD=1, TRACE> (variant 4; TRACE = 1 is
+# the wave-trace build picked only while rt_set_wave_trace holds a buffer)
 def _v3(t, p, c, wd=0):
     w = 8 if (c and not t and not wd) else 1
     return f"_ZN2rt3dev16render_kernel_v3ILb0ELi{w}ELb{t}ELb{p}ELb{c}ELb{wd}EEEvNS0_7KParamsE"
 
 
-def _v4(t, p, wd=0):
-    return f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}ELb{wd}ELi1EEEvNS0_7KParamsE"
+def _v4(t, p, wd=0, trace=0):
+    return f"_ZN2rt3dev16render_kernel_v4ILb0ELb{t}ELi2ELb{p}ELb{wd}ELi1ELb{trace}EEEvNS0_7KParamsE"
 
 
 HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + [_v4(t, p) for t in (0, 1) for p in (0, 1)] + \
@@ -47,7 +48,7 @@ def kernel_metadata(tmp_path):
                            capture_output=True, text=True).stdout
     meta, name = {}, None
     for line in notes.splitlines():
-        m = re.match(r"\s+\.(name|private_segment_fixed_size|vgpr_count|vgpr_spill_count):\s+(\S+)", line)
+        m = re.match(r"\s+\.(name|private_segment_fixed_size|vgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\S+)", line)
         if not m:
             continue
         if m.group(1) == "name":
@@ -71,9 +72,9 @@ def test_hot_kernels_register_and_scratch_budget(tmp_path):
     assert meta[_v3(0, 1, 1)]["vgpr_count"] <= 64
 
 
-def _flat(t, p, persistent=False):
+def _flat(t, p, persistent=False, trace=0):
     if persistent:
-        return f"_ZN2rt3dev29render_kernel_flat_persistentILb0ELb{t}ELb{p}ELi1EEEvNS0_7KParamsE"
+        return f"_ZN2rt3dev29render_kernel_flat_persistentILb0ELb{t}ELb{p}ELi1ELb{trace}EEEvNS0_7KParamsE"
     return f"_ZN2rt3dev18render_kernel_flatILb0ELb{t}ELb{p}ELi{8 if not t else 1}EEEvNS0_7KParamsE"
 
 
@@ -91,3 +92,10 @@ def test_flat_kernels_register_and_scratch_budget(tmp_path):
                 assert meta[k]["private_segment_fixed_size"] <= 192, (k, meta[k])
     assert meta[_flat(0, 0)]["vgpr_count"] <= 64
     assert meta[_flat(0, 1)]["vgpr_count"] <= 64
+    # the persistent kernels' wave-trace builds exist beside the product builds, which carry none of the trace's
+    # registers: the textured XORWOW persistent flat kernel (C5) spilled 105 SGPRs to VGPR lanes with the run-time
+    # checked trace, 26 now (profiles/r05q_ab_c5_trace_build.txt)
+    for t in (0, 1):
+        for p in (0, 1):
+            assert _flat(t, p, True, trace=1) in meta and _v4(t, p, trace=1) in meta
+    assert meta[_flat(1, 0, True)]["sgpr_spill_count"] <= 40, meta[_flat(1, 0, True)]
