@@ -2992,10 +2992,14 @@ thread_local int g_regen_live_frac = 48;
 // and no cap: profiles/r03r_ab_leaf_break.txt)
 thread_local int g_leaf_break = 3;
 // RT_TUNE_FLAT_MAX: scenes of at most this many primitives run the flat kernels (variants 5, 6) where the automatic
-// choice would run v3 / v4.  RT_TUNE_RIUS_TRIPS: their RandomInUnitSphere attempts per pass before a rejecting lane
-// defers the rest of the call to the next pass (0 = unbounded)
+// choice would run v3 / v4.  RT_TUNE_RIUS_TRIPS: the tile flat kernel's RandomInUnitSphere attempts per pass before a
+// rejecting lane defers the rest of the call to the next pass (0 = unbounded; 4: C3's optimum, a wave otherwise runs
+// the loop as long as its unluckiest lane).  RT_TUNE_RIUS_TRIPS_PERSISTENT: the same for the persistent flat kernel,
+// unbounded by default — a C5 frame is bound by its last pixels' chains of passes, and a deferred call adds a pass to
+// one (C5 0.262 -> 0.253 ms per step unbounded, K = 4 / 6 / 8: 0.262 / 0.260 / 0.255; profiles/r05u_c5_rius_trips.txt)
 thread_local int g_flat_max = 16;
 thread_local int g_rius_trips = 4;
+thread_local int g_rius_trips_persistent = 0;
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
@@ -3331,13 +3335,14 @@ int rt_set_tuning(int key, int value) {
         g_leaf_break = value;
         return prev;
     }
-    if (key == RT_TUNE_RIUS_TRIPS) {
+    if (key == RT_TUNE_RIUS_TRIPS || key == RT_TUNE_RIUS_TRIPS_PERSISTENT) {
         if (value < 0 || value > 64) {
             set_error("rt_set_tuning: RandomInUnitSphere trips must be in [0, 64]");
             return RT_ERR_INVALID_ARGUMENT;
         }
-        int prev = g_rius_trips;
-        g_rius_trips = value;
+        int& knob = key == RT_TUNE_RIUS_TRIPS ? g_rius_trips : g_rius_trips_persistent;
+        int prev = knob;
+        knob = value;
         return prev;
     }
     if (key == RT_TUNE_FLAT_MAX) {
@@ -3627,7 +3632,8 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.flat_runs[0] = S.flat_runs[0];
         P.flat_runs[1] = S.flat_runs[1];
     }
-    P.rius_cap = g_rius_trips > 0 ? (uint32_t)g_rius_trips : 0xffffffffu;  // (the flat kernels')
+    const int rius_trips = V.kernel == 6 ? g_rius_trips_persistent : g_rius_trips;  // (the flat kernels')
+    P.rius_cap = rius_trips > 0 ? (uint32_t)rius_trips : 0xffffffffu;
     const uint32_t tile = V.block == 64 ? 8u : 16u;  // v2/v3/v4: one 8×8 tile per wave
     P.tiles_x = (a->width + tile - 1) / tile;
     const uint32_t tiles = P.tiles_x * ((T.local_rows + tile - 1) / tile);

@@ -373,10 +373,11 @@ int rt_last_variant(void);
  *   geometry) where the automatic choice would run variant 3 or 4; so do scenes of up to 64 primitives in which a
  *   rectangle's reference box touches another primitive's (coplanar, abutting or meeting rectangles, a sphere on a
  *   floor), unless the value is 0.  The BVH kernels return the geometric closest hit, which differs from the
- *   reference's only on exact ties and hits within rounding of a reference box face.  RT_TUNE_RIUS_TRIPS: the flat
- *   kernels make at most this many RandomInUnitSphere attempts (Math.cuh:252-260) per shading pass; a lane whose
- *   attempts were all rejected continues the same call at the wave's next pass (0 = unbounded; 0..64; default 4;
- *   Philox mode rounds it up to whole blocks of four attempts).  It does not change the image.
+ *   reference's only on exact ties and hits within rounding of a reference box face.  RT_TUNE_RIUS_TRIPS: the tile
+ *   flat kernel (variant 5) makes at most this many RandomInUnitSphere attempts (Math.cuh:252-260) per shading pass; a
+ *   lane whose attempts were all rejected continues the same call at the wave's next pass (0 = unbounded; 0..64;
+ *   default 4; Philox mode rounds it up to whole blocks of four attempts).  RT_TUNE_RIUS_TRIPS_PERSISTENT: the same for
+ *   the persistent flat kernel (variant 6; default 0 = unbounded: C5 -3.5 %).  Neither changes the image.
  *   RT_TUNE_QUEUE_PREFETCH: the persistent kernels (variants 4, 6) fetch their next chunk of work indices (the queue
  *   atomic) ahead, once at most this many indices of the current chunk are left, so the atomic's round trip overlaps
  *   the wave's work (0 = off: fetched when the chunk runs out; 0..64; default 32: C5 -7 %,
@@ -389,7 +390,7 @@ enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
                      RT_TUNE_REGEN_LIVE_FRAC = 9, RT_TUNE_LEAF_BREAK = 10, RT_TUNE_RIUS_TRIPS = 11,
                      RT_TUNE_FLAT_MAX = 12, RT_TUNE_QUEUE_PREFETCH = 13, RT_TUNE_QUEUE_GUIDE = 14,
-                     RT_TUNE_QUEUE_MIN_CHUNK = 15 };
+                     RT_TUNE_QUEUE_MIN_CHUNK = 15, RT_TUNE_RIUS_TRIPS_PERSISTENT = 16 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

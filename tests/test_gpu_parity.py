@@ -862,7 +862,8 @@ def test_persistent_queue_knobs_change_schedule_not_pixels(chunk, stride):
 # scheduling knobs (rt_hip.h) and the kernels they steer: (key, value) pairs around the defaults, with the extremes
 V3_KNOBS = [(abi.RT_TUNE_LEAF_BREAK, k, v) for k in (0, 1, 64) for v in (2, 3)] + \
            [(abi.RT_TUNE_REGEN_LIVE_FRAC, k, v) for k in (0, 1, 64) for v in (2, 3)] + \
-           [(abi.RT_TUNE_RIUS_TRIPS, k, v) for k in (0, 1, 2, 3, 5) for v in (5, 6)]
+           [(abi.RT_TUNE_RIUS_TRIPS, k, v) for k in (0, 1, 2, 3, 5) for v in (5, 6)] + \
+           [(abi.RT_TUNE_RIUS_TRIPS_PERSISTENT, k, 6) for k in (0, 1, 3, 4)]
 
 
 @pytest.mark.parametrize("key, value, variant", V3_KNOBS, ids=lambda v: str(v))

@@ -216,7 +216,8 @@ def test_scheduling_knobs_defaults_and_ranges():
     previous value returned (include/rt_hip.h rt_tuning_key)."""
     L = lib()
     for key, default, bad in [(abi.RT_TUNE_REGEN_THRESHOLD, 56, [0, 65]), (abi.RT_TUNE_REGEN_LIVE_FRAC, 48, [-1, 65]),
-                              (abi.RT_TUNE_LEAF_BREAK, 3, [-1, 65])]:
+                              (abi.RT_TUNE_LEAF_BREAK, 3, [-1, 65]), (abi.RT_TUNE_RIUS_TRIPS, 4, [-1, 65]),
+                              (abi.RT_TUNE_RIUS_TRIPS_PERSISTENT, 0, [-1, 65])]:
         prev = L.rt_set_tuning(key, 7)
         assert prev == default, (key, prev)
         assert L.rt_set_tuning(key, prev) == 7
