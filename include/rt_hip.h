@@ -307,7 +307,9 @@ float rt_last_launch_host_ms(void);
  * (100 MHz): v3 and flat, 2 per 8×8 tile (its wave's start and end; tools/wave_timeline.py); v4 and persistent flat,
  * 8 per persistent wave (start, the moment its work queue ran dry, end, pixels taken, HW_REG_HW_ID | XCC id << 32,
  * when it last handed out a pixel, chunk grabs | exhausted-head probes << 32, ticks spent waiting for queue atomics;
- * tools/v4_timeline.py).  Stamps that would fall beyond `words` are not written.  NULL = off. */
+ * tools/v4_timeline.py).  Stamps that would fall beyond `words` are not written.  NULL = off.  The persistent kernels
+ * run a separate trace build while a buffer is set (the product build carries no stamps); RT_FLAG_COUNT_TESTS
+ * launches of them run the counting build, which writes no per-wave records. */
 int rt_set_wave_trace(void* buffer, uint64_t words);
 
 /* Experiment (per thread): device uint32 permutation of the frame's 8×8 tiles giving the v3 kernels' launch
