@@ -47,6 +47,12 @@ for v in (int(x) for x in args.variants.split(",")):
            "ltr": args.ltr, "variant": v, "ran": lib().rt_last_variant(), "pixels": int(img.size),
            "pixels_differ": int(len(bad)), "rays": int(r.counters[0]), "oracle_rays": int(cnt.rays),
            "oracle_s": round(oracle_s, 1), "first_differ": [[int(y), int(x)] for y, x in bad[:6]]}
+    if len(bad):  # how far the differing pixels are off: RGBA8 channel differences (north_star's per-channel tolerance)
+        a8 = img[bad[:, 0], bad[:, 1]].view(np.uint8).reshape(-1, 4)[:, :3].astype(np.int32)
+        b8 = ref[bad[:, 0], bad[:, 1]].view(np.uint8).reshape(-1, 4)[:, :3].astype(np.int32)
+        d = np.abs(a8 - b8)
+        out["max_channel_diff"] = int(d.max())
+        out["channel_diff_hist"] = {int(k): int(c) for k, c in zip(*np.unique(d.max(axis=1), return_counts=True))}
     if not philox:
         out["states_differ"] = int((r.states()[:, :6] != st[:, :6]).any(axis=1).sum())
     print(json.dumps(out), flush=True)
