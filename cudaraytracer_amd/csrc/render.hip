@@ -2542,8 +2542,10 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
         }
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
-            flat_trace<COUNT_TESTS>(prims, P.ref_nodes, P.flat_boxes, P.num_prims, P.flat_runs[0], P.flat_runs[1], ro, rd, hit,
-                                    tag, t, cnt);
+            // the scan's launch-uniform operands re-read per pass (as the persistent flat kernel's)
+            KParamsC* const q = kparams_reload();
+            flat_trace<COUNT_TESTS>(q->prims, q->ref_nodes, q->flat_boxes, q->num_prims, q->flat_runs[0], q->flat_runs[1], ro,
+                                    rd, hit, tag, t, cnt);
             mode = MODE_SHADE;
         }
         const uint64_t c1 = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
