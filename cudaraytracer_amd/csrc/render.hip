@@ -616,7 +616,7 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, con
         float cosine;
         if (y_len != 0.0f && fabsf(cn) >= 0x1p-100f) cosine = div_rn(cn, len, y_len);
         else cosine = cn / len;
-        if (exiting) cosine = sqrtf(1.0f - ir * ir * (1 - cosine * cosine));
+        if (exiting) cosine = sqrt_fast(1.0f - ir * ir * (1 - cosine * cosine));  // (= sqrtf bit for bit)
         const float ni_over_nt = exiting ? ir : m1.x;
         const f3 outward_normal = exiting ? neg(normal) : normal;
         // Refract (Math.cuh:292-304): uv = UnitVector(v)
@@ -633,7 +633,7 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, con
         if (refl) {
             rd = reflect(rd, normal);
         } else if (discriminant > 0) {
-            rd = sub(scale(ni_over_nt, sub(ud, scale(dt, outward_normal))), scale(sqrtf(discriminant), outward_normal));
+            rd = sub(scale(ni_over_nt, sub(ud, scale(dt, outward_normal))), scale(sqrt_fast(discriminant), outward_normal));
         } else {
             rd = mk(0.0f, 0.0f, 0.0f);  // uninitialised `refracted` in the reference (ξ = 1.0, TIR)
         }
