@@ -451,43 +451,60 @@ __device__ __forceinline__ float rt_atan2f(const float y, const float x) {
     return __builtin_signbit(y) ? -r : r;
 }
 
-// Texture::value (Texture.cuh:42-45, 58-67, 83-105)
+// Texture::value (Texture.cuh:42-45, 58-67, 83-105) in two steps: texture_fetch returns the colour, or for an image the
+// address of the texel, texture_gather loads it as one dword and texture_resolve turns it into the colour.  shade()
+// issues the gather for every lane of its Lambertian / Metal path (a lane without a texel reads a dummy word) and
+// resolves it after RandomInUnitSphere: no branch between the load and its use, so the compiler waits for it only
+// there and the round trip overlaps the rejection loop.  Each image is followed by >= 4 spare bytes (scene_build.cpp):
+// the RGB8 layout's dword reads one byte past its texel, which the colour ignores.
+struct TexFetch {
+    f3 color;              // the colour, unless pending
+    const uint8_t* texel;  // pending: the texel's first byte
+    bool pending;
+};
+__device__ __forceinline__ TexFetch texture_fetch(const float4& m0, const float4& m1, const float4& m2, uint32_t tex_type,
+                                                  float u, float v, f3 p, const int4* __restrict__ imgs,
+                                                  const uint8_t* __restrict__ texels) {
+    TexFetch f{mk(0.0f, 0.0f, 0.0f), nullptr, false};
+    if (tex_type == RT_CONSTANT) {
+        f.color = xyz(m1);
+    } else if (tex_type == RT_CHECKER) {
+        const float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+        f.color = sines < 0 ? xyz(m1) : xyz(m2);
+    } else if (tex_type == RT_IMAGE) {
+        const int img = __float_as_int(m0.w);
+        const int4 im = img < 0 ? make_int4(-1, 0, 0, 0) : imgs[img];  // (byte offset of the texels, width, height,
+                                                                      //  bytes per texel)
+        if (im.x < 0) {  // no image / data == nullptr (Texture.cuh:83-84) → cyan
+            f.color = mk(0.0f, 1.0f, 1.0f);
+        } else {
+            u = clampf(u, 0.0f, 1.0f);
+            v = 1.0f - clampf(v, 0.0f, 1.0f);
+            int i = (int)(u * (float)im.y);
+            int j = (int)(v * (float)im.z);
+            if (i >= im.y) i = im.y - 1;
+            if (j >= im.z) j = im.z - 1;
+            // RGBA8-padded layout: 4 bytes per texel; the reference's RGB8 layout (Texture.cuh:76, 96-104): 3
+            f.texel = texels + im.x + ((size_t)j * (size_t)im.y + (size_t)i) * (size_t)im.w;
+            f.pending = true;
+        }
+    }
+    return f;
+}
+__device__ __forceinline__ uint32_t texture_gather(const TexFetch& f, const void* dummy) {
+    return *reinterpret_cast<const uint32_t*>(f.pending ? f.texel : reinterpret_cast<const uint8_t*>(dummy));
+}
+__device__ __forceinline__ f3 texture_resolve(const TexFetch& f, uint32_t w) {
+    if (!f.pending) return f.color;
+    const float color_scale = 1.0f / 255.0f;
+    return mk(color_scale * (float)(w & 0xffu), color_scale * (float)((w >> 8) & 0xffu),
+              color_scale * (float)((w >> 16) & 0xffu));
+}
 __device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, const float4& m2, uint32_t tex_type,
                                             float u, float v, f3 p, const int4* __restrict__ imgs,
                                             const uint8_t* __restrict__ texels) {
-    if (tex_type == RT_CONSTANT) return xyz(m1);
-    if (tex_type == RT_CHECKER) {
-        const float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
-        return sines < 0 ? xyz(m1) : xyz(m2);
-    }
-    if (tex_type == RT_IMAGE) {
-        const int img = __float_as_int(m0.w);
-        if (img < 0) return mk(0.0f, 1.0f, 1.0f);  // no image (Texture.cuh:83-84: data == nullptr → cyan)
-        const int4 im = imgs[img];  // (byte offset of the texels, width, height, bytes per texel)
-        if (im.x < 0) return mk(0.0f, 1.0f, 1.0f);  // data == nullptr
-        u = clampf(u, 0.0f, 1.0f);
-        v = 1.0f - clampf(v, 0.0f, 1.0f);
-        int i = (int)(u * (float)im.y);
-        int j = (int)(v * (float)im.z);
-        if (i >= im.y) i = im.y - 1;
-        if (j >= im.z) j = im.z - 1;
-        const float color_scale = 1.0f / 255.0f;
-        const size_t texel = (size_t)j * (size_t)im.y + (size_t)i;
-        uint32_t r, g, b;
-        if (im.w == 4) {  // RGBA8-padded layout: one dword gather per texel
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(texels + im.x + texel * 4);
-            r = w & 0xffu;
-            g = (w >> 8) & 0xffu;
-            b = (w >> 16) & 0xffu;
-        } else {  // the reference's RGB8 layout (Texture.cuh:76, 96-104): three byte gathers
-            const uint8_t* px = texels + im.x + texel * 3;
-            r = px[0];
-            g = px[1];
-            b = px[2];
-        }
-        return mk(color_scale * (float)r, color_scale * (float)g, color_scale * (float)b);
-    }
-    return mk(0.0f, 0.0f, 0.0f);
+    const TexFetch f = texture_fetch(m0, m1, m2, tex_type, u, v, p, imgs, texels);
+    return f.pending ? texture_resolve(f, *reinterpret_cast<const uint32_t*>(f.texel)) : f.color;
 }
 
 __device__ __forceinline__ uint32_t f2u8(float f) { return f != f ? 0u : (uint32_t)(int)f; }
@@ -643,19 +660,19 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, con
     // The attenuation (texture lookup) before the rejection loop, which it does not depend on: an image texel's gather
     // is in flight while RandomInUnitSphere runs instead of after it (no RNG draw moves)
     const float4 m1 = mats[3 * mat + 1];
-    f3 attenuation;
-    if (!TEX || ttype == RT_CONSTANT) {
-        attenuation = xyz(m1);
-    } else {
+    TexFetch tex{xyz(m1), nullptr, false};
+    if (TEX && ttype != RT_CONSTANT) {
         const float4 m2 = mats[3 * mat + 2];
-        attenuation = texture_value(m0, m1, m2, ttype, hu, hv, p, imgs, P->texels);
+        tex = texture_fetch(m0, m1, m2, ttype, hu, hv, p, imgs, P->texels);
     }
+    const uint32_t texel_word = TEX ? texture_gather(tex, P->prims) : 0u;  // (a dummy word of the primitive table)
     f3 q;
     if constexpr (DEFER) {
         if (!random_in_unit_sphere_capped(rng, rtl, P->rius_cap, q)) return SHADE_DEFERRED;
     } else {
         q = random_in_unit_sphere(rng, rtl);
     }
+    const f3 attenuation = texture_resolve(tex, texel_word);
     bool ok = true;
     if (mtype == RT_LAMBERTIAN) {  // Lambertian::Scatter (Material.cuh:43-62)
         const f3 target = add(add(p, normal), q);

@@ -415,8 +415,10 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         out->imgs.push_back(im.width);
         out->imgs.push_back(im.height);
         out->imgs.push_back(bpt);
+        // (each image is followed by at least 4 spare bytes: the kernels gather a texel as one dword, which for the
+        // RGB8 layout's last texel reads one byte past it; then 16-B alignment)
         if (bytes && !with_texels) {
-            off = (off + bytes + 15) & ~(size_t)15;
+            off = (off + bytes + 4 + 15) & ~(size_t)15;
         } else if (bytes) {
             out->texels.resize(off + bytes);
             uint8_t* dst = out->texels.data() + off;
@@ -430,7 +432,7 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
                     dst[4 * t + 3] = 0;
                 }
             }
-            off += bytes;
+            off += bytes + 4;
             off = (off + 15) & ~(size_t)15;
             out->texels.resize(off, 0);
         }
