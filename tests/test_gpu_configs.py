@@ -249,6 +249,34 @@ def test_image_texture_without_image_is_cyan(variant):
 
 
 @pytest.mark.parametrize("layout", [3, 4])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6])
+def test_tiny_images_every_texel_including_the_last(variant, layout):
+    """Images of 1x1, 3x1 and 2x3 texels (odd byte sizes in the RGB8 layout): every lane's texel is gathered as one
+    dword, so the last texel of the last image reads one byte past it into the image's padding (scene_build.cpp) —
+    the colours must still be the oracle's, in both texel layouts and on every kernel that shades textures."""
+    from cudaraytracer_amd._lib import lib
+    cfg = scenes.CONFIGS["c5"].scaled(96, 64, 4)
+    rng = np.random.default_rng(7)
+    imgs = [rng.integers(0, 256, size=sh, dtype=np.uint8) for sh in ((1, 1, 3), (1, 3, 3), (3, 2, 3))]
+    sc = scenes.builtin(cfg.scene, images=imgs)
+    prev = lib().rt_set_tuning(6, layout)
+    lib().rt_set_variant(variant)
+    try:
+        ds = DeviceScene(sc)
+        r = Renderer(cfg.width, cfg.height)
+        r.render_init()
+        r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
+        torch.cuda.synchronize()
+    finally:
+        lib().rt_set_tuning(6, prev)
+        lib().rt_set_variant(-1)
+    st = po.init_states(cfg.width, cfg.height)
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
+    np.testing.assert_array_equal(r.image(), ref)
+    np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
+
+
+@pytest.mark.parametrize("layout", [3, 4])
 def test_texel_layouts_give_the_same_image(layout, c5_scene):
     """RGB8 (the reference's 3-byte texels) and RGBA8-padded device layouts render identical images."""
     from cudaraytracer_amd._lib import lib
