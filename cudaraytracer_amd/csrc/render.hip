@@ -1967,7 +1967,7 @@ __device__ __forceinline__ bool work_pixel(const KParams& P, uint32_t idx, uint3
 // are split over kQueueCounters heads, each owning a contiguous range; a wave draws chunks from its head with one
 // atomic each and moves on to the next live head when its own is exhausted.  Chunks are P.work_chunk indices while
 // the head had plenty left at this wave's last grab, then 64 (other waves draining the same head make that count
-// stale, so a chunk above 64 can still lengthen the frame's tail: RT_TUNE_QUEUE_CHUNK defaults to 64).
+// stale, so a chunk above 64 can still lengthen the frame's tail: RT_TUNE_QUEUE_CHUNK defaults to 128).
 // TRACE: the wave-trace build (a persistent kernel's instance picked only while rt_set_wave_trace holds a buffer); the
 // product instances carry none of the trace's stamps and counters, whose SGPRs spilled to VGPR lanes (C5 kernel: 105
 // spilled SGPRs with them, 53 without; -2.5 % per frame, profiles/r05q_ab_c5_trace_build.txt).
@@ -3116,7 +3116,10 @@ constexpr size_t kFlatTabLdsMax = 16 * 1024;  // LDS per persistent flat wave fo
 constexpr uint32_t kQueueSlots = 256;
 constexpr uint32_t kQueueMaxStride = 4096;  // bytes between heads (RT_TUNE_QUEUE_STRIDE)
 thread_local int g_queue_stride = 128;  // RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's queue heads
-thread_local int g_queue_chunk = 64;    // RT_TUNE_QUEUE_CHUNK: work indices per queue atomic
+// RT_TUNE_QUEUE_CHUNK: work indices per queue atomic while the head has plenty left.  128 since the texel gather
+// overlaps RandomInUnitSphere: C5 -3.6 % against 64 (0.2525 vs 0.2620 ms, 6 alternations; 192 / 256 lose,
+// profiles/r05ag_c5_queue_chunk.txt); round 3 had measured 64..256 within 3 %
+thread_local int g_queue_chunk = 128;
 thread_local int g_queue_prefetch = 32; // RT_TUNE_QUEUE_PREFETCH: fetch the next chunk ahead at this many indices left
 thread_local int g_queue_guide = 0;     // RT_TUNE_QUEUE_GUIDE: guided chunks, head_left / (waves per head × this)
 thread_local int g_queue_min = 16;      // RT_TUNE_QUEUE_MIN_CHUNK: the guided chunks' floor

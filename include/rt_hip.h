@@ -360,10 +360,10 @@ int rt_last_variant(void);
  *   the per-tile wave lifetimes the previous launch on the same stream with the same tile grid measured;
  *   0 = row-major.  The image does not depend on it. */
 /*   RT_TUNE_TEXEL_LAYOUT: device bytes per texel of the images of later rt_scene_create calls: 3 (default,
- *   the reference's RGB8 layout, Texture.cuh:76: three byte gathers per lookup) or 4 (RGBA8-padded: one dword
- *   gather per lookup, 4/3 the memory).  The image does not depend on it. */
+ *   the reference's RGB8 layout, Texture.cuh:76) or 4 (RGBA8-padded, 4/3 the memory); the kernels gather one dword
+ *   per lookup in either.  The image does not depend on it. */
 /*   RT_TUNE_QUEUE_CHUNK: work indices (pixels) a persistent (v4) wave takes from its queue head per atomic
- *   (a multiple of 64 in [64, 4096], default 64).  RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's 16
+ *   (a multiple of 64 in [64, 4096], default 128; 64 near a head's end).  RT_TUNE_QUEUE_STRIDE: bytes between the v4 kernel's 16
  *   queue heads (a power of two in [128, 4096], default 128).  Neither changes the image.
  *   RT_TUNE_REGEN_LIVE_FRAC: the v3 kernels cap the regeneration threshold at this fraction (x/64) of the wave's
  *   pixels still rendering (0 = off; 0..64; default 48).  The image does not depend on it.

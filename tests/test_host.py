@@ -230,7 +230,7 @@ def test_queue_knobs_defaults_and_ranges():
     """rt_set_tuning for the persistent kernels' queue (CPU: no kernel runs): chunk (multiple of 64), head stride
     (power of two), chunk prefetch threshold (include/rt_hip.h RT_TUNE_QUEUE_PREFETCH)."""
     L = lib()
-    for key, default, good, bad in [(abi.RT_TUNE_QUEUE_CHUNK, 64, 128, [0, 96, 4160]),
+    for key, default, good, bad in [(abi.RT_TUNE_QUEUE_CHUNK, 128, 192, [0, 96, 4160]),
                                     (abi.RT_TUNE_QUEUE_STRIDE, 128, 4096, [64, 192, 8192]),
                                     (abi.RT_TUNE_QUEUE_PREFETCH, QUEUE_PREFETCH_DEFAULT, 48, [-1, 65]),
                                     (abi.RT_TUNE_QUEUE_GUIDE, QUEUE_GUIDE_DEFAULT, 4, [-1, 65]),
