@@ -221,7 +221,7 @@ static void outputs_and_misc() {
     CHECK(rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 96) == RT_ERR_INVALID_ARGUMENT);
     CHECK(rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 192) == RT_ERR_INVALID_ARGUMENT);
     CHECK(rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 8192) == RT_ERR_INVALID_ARGUMENT);
-    CHECK(rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 128) == 64 && rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 64) == 128);
+    CHECK(rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 192) == 128 && rt_set_tuning(RT_TUNE_QUEUE_CHUNK, 128) == 192);
     CHECK(rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 4096) == 128 && rt_set_tuning(RT_TUNE_QUEUE_STRIDE, 128) == 4096);
     CHECK(rt_render(nullptr, nullptr, nullptr) == RT_ERR_INVALID_ARGUMENT);
     const int dev0 = 0;
