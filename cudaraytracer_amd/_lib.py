@@ -20,6 +20,8 @@ EXPORTED = [
     "LaunchRenderInit",
     "rt_last_error",
     "rt_version",
+    "rt_abi_version",
+    "rt_set_launch_flags",
     "rt_set_device",
     "rt_scene_create",
     "rt_scene_from_reference_graph",
@@ -70,6 +72,7 @@ def _declare(lib: C.CDLL) -> None:
     vp = C.c_void_p
     lib.rt_last_error.restype = C.c_char_p
     lib.rt_version.restype = C.c_char_p
+    lib.rt_set_launch_flags.argtypes = [C.c_uint32]
     lib.rt_set_device.argtypes = [C.c_int]
     lib.rt_scene_create.argtypes = [P(abi.SceneDesc), P(vp)]
     lib.rt_scene_from_reference_graph.argtypes = [vp, P(vp)]

@@ -65,6 +65,9 @@ static void free_device(DeviceScene* s) {
     if (s->ref_nodes) (void)hipFree((void*)s->ref_nodes);
     if (s->flat_boxes) (void)hipFree((void*)s->flat_boxes);
     s->prims_flat = s->ref_nodes = s->flat_boxes = nullptr;
+    if (s->bvh_ref_nodes) (void)hipFree((void*)s->bvh_ref_nodes);
+    if (s->bvh_boxes) (void)hipFree((void*)s->bvh_boxes);
+    s->bvh_ref_nodes = s->bvh_boxes = nullptr;
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);  // texels: owned by rt_scene::texel_block
     s->nodes = s->prims = s->mats = nullptr;
@@ -94,7 +97,10 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.ref_nodes = p;
     if ((rc = upload(h.flat_boxes, &p, "hipMalloc/hipMemcpy(flat_boxes)"))) goto fail;
     d.flat_boxes = p;
-    d.touching_rects = h.touching_rects;
+    if ((rc = upload(h.bvh_ref_nodes, &p, "hipMalloc/hipMemcpy(bvh_ref_nodes)"))) goto fail;
+    d.bvh_ref_nodes = p;
+    if ((rc = upload(h.bvh_boxes, &p, "hipMalloc/hipMemcpy(bvh_boxes)"))) goto fail;
+    d.bvh_boxes = p;
     d.flat_runs[0] = h.flat_runs[0];
     d.flat_runs[1] = h.flat_runs[1];
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
@@ -115,8 +121,9 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.depth = h.depth;
     d.has_image_textures = h.has_image_textures;
     d.has_textures = h.has_textures;
+    d.has_rects = h.has_rects;
     d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs.size() + h.prims.size() + h.prims_flat.size() + h.ref_nodes.size() +
-                      h.flat_boxes.size() + h.mats.size()) * 4 +
+                      h.flat_boxes.size() + h.bvh_ref_nodes.size() + h.bvh_boxes.size() + h.mats.size()) * 4 +
                      h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;
@@ -364,6 +371,7 @@ extern "C" {
 const char* rt_last_error(void) { return g_last_error.c_str(); }
 
 const char* rt_version(void) { return "librt_hip 0.1 (gfx950)"; }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 int rt_set_device(int device) {
     hipError_t e = hipSetDevice(device);

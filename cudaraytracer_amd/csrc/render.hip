@@ -24,6 +24,7 @@
 
 #include <cfloat>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <atomic>
 #include <map>
@@ -259,6 +260,9 @@ struct KParams {
     const float4* ref_nodes;         // flat kernel: the reference BVH over the flat table (ref_trace)
     const float4* flat_boxes;        // flat kernel: per flat record its reference box (flat_trace's exactness check)
     uint32_t flat_runs[2];           // flat kernel: [begin, end) of each primitive type's run in the flat table
+    const float4* bvh_ref_nodes;     // BVH kernels: the reference BVH over `prims` (bvh_clear), NULL = no replay
+    const float4* bvh_boxes;         // BVH kernels: per `prims` record its reference box (bvh_clear)
+    uint32_t bvh_has_rects;          // BVH kernels: the scene holds a rectangle (bvh_clear's check of misses)
 };
 
 constexpr int kStackMax = 64;
@@ -288,6 +292,7 @@ struct Counts {
     uint32_t rays, boxes, prims, primary;
     uint32_t wnode, wleaf, wshade;  // COUNT_TESTS: wave-level iterations (counted on the first active lane)
     uint32_t rects = 0;  // COUNT_TESTS: the part of `prims` that are rectangle tests (12 FLOP vs a sphere's 23)
+    uint32_t replays = 0;  // COUNT_TESTS: rays whose closest hit the exactness check sent through the reference BVH
     uint32_t wnode_uniform = 0, wleaf_uniform = 0;  // COUNT_TESTS (v3): ... of them with one node / primitive
     uint64_t ctrav = 0, cshade = 0, ctotal = 0, cleaf = 0;  // COUNT_TESTS (v3): wave clock cycles per phase
     // COUNT_TESTS (v3): idle lanes summed over node iterations: pixel done / ray finished, waiting for the
@@ -309,6 +314,12 @@ constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX
 // relative 2^-20 (≥ 2·(3·2^-24)): a box the exact ray meets is never culled, whatever the camera distance.
 // (Widening only adds box visits; the closest hit is decided by the exact primitive tests.)
 constexpr float kSlabSlack = 1.0f + 0x1p-20f;
+// A hit index with this bit set (bvh_clear): a primitive tied with the closest hit so far (indices are < 2^26)
+constexpr int kTieBit = 0x40000000;
+#ifndef RT_BVH_EXACT
+#define RT_BVH_EXACT 1  // (A/B builds only: 0 = the BVH kernels without the reference replay, the round-5 kernels;
+                        //  2 = the tie tracking and the check without the replay; 3 = the tie tracking alone)
+#endif
 
 // Closest hit (BVHNode::Hit, Hittable.cuh:387-439, and the primitive tests of PerformHit :470-485).
 // Returns the primitive index (BVH order) or -1, and the hit distance in t_best.
@@ -387,10 +398,13 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
                         t_best = t;
                         hit = (int)i;
                     } else {
+                        const bool tied = t == t_best;  // (bvh_clear: a tie at the closest hit so far)
                         t = (-b + sq) / a_dd;
                         if (t < t_best && t > kTmin) {
                             t_best = t;
                             hit = (int)i;
+                        } else if (tied || t == t_best) {
+                            hit |= kTieBit;
                         }
                     }
                 }
@@ -404,8 +418,8 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
                     const float x = oa + t * da;
                     const float y = ob + t * db;
                     if (!(x < p0.y || x > p0.z || y < p0.w || y > p1.x)) {
+                        hit = t == t_best ? (int)i | kTieBit : (int)i;  // (a rectangle re-accepts an equal t)
                         t_best = t;
-                        hit = (int)i;
                     }
                 }
             }
@@ -416,6 +430,281 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
     return hit;
 }
 
+// The reference's own closest-hit query, replayed exactly: BVHNode::Hit (Hittable.cuh:387-439) over the tree the
+// BVHNode constructor builds (ref_nodes, scene_build.cpp), with AABB::Hit (AABB.cuh:30-50) on the reference's boxes and
+// its t_max bookkeeping (a node's box is tested against the closest hit as of its push).  Per lane, with a private
+// stack: the flat kernel runs it only for the rare rays whose answer box culling could change (flat_trace).
+constexpr int kRefStack = 16;     // > kRefTreeMaxDepth (rt_internal.h): the flat kernels' replay
+constexpr int kRefStackBvh = 32;  // > kRefTreeMaxDepthBvh: the BVH kernels' (bvh_clear)
+__device__ __forceinline__ bool ref_box(const float4 lo, const float4 hi, const f3 o, const f3 inv, float t_max) {
+    float t_min = kTmin;
+    const float los[3] = {lo.x, lo.y, lo.z}, his[3] = {hi.x, hi.y, hi.z};
+    const float os[3] = {o.x, o.y, o.z}, invs[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        float t0 = (los[a] - os[a]) * invs[a];
+        float t1 = (his[a] - os[a]) * invs[a];
+        if (invs[a] < 0.0f) {
+            const float tmp = t0;
+            t0 = t1;
+            t1 = tmp;
+        }
+        t_min = t0 > t_min ? t0 : t_min;
+        t_max = t1 < t_max ? t1 : t_max;
+        if (t_max <= t_min) return false;
+    }
+    return true;
+}
+struct HitOut {
+    int hit;
+    uint32_t tag;
+    float t;
+};
+// (not inlined: the kernels' registers are sized for their common path; the result comes back in registers)
+template <int STK>
+__device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, const float4* __restrict__ prims, const f3 o,
+                                         const f3 d) {
+    int hit = -1;
+    uint32_t tag = 0u;
+    float t_best = FLT_MAX;  // = rec.t once something is hit (the reference's "hit_something ? rec.t : t_max")
+    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float a_dd = dot(d, d);
+    int stk[STK];
+    float stm[STK];
+    if (!ref_box(rnodes[0], rnodes[1], o, inv, FLT_MAX)) return HitOut{hit, tag, t_best};  // its own box first (:389)
+    int top = 0;
+    stk[0] = 0;
+    stm[0] = FLT_MAX;
+    while (top >= 0) {
+        const int n = stk[top];
+        const float tm = stm[top];
+        top--;
+        const float4 lo = rnodes[2 * n], hi = rnodes[2 * n + 1];
+        if (!ref_box(lo, hi, o, inv, tm)) continue;
+        const int ch[2] = {__float_as_int(lo.w), __float_as_int(hi.w)};
+        for (int k = 0; k < 2; k++) {
+            if (ch[k] >= 0) {
+                top++;
+                stk[top] = ch[k];
+                stm[top] = t_best;
+                continue;
+            }
+            const int i = ~ch[k];  // PerformHit (Hittable.cuh:470-485) with t_max = the closest hit so far
+            const float4 q0 = prims[2 * i], q1 = prims[2 * i + 1];
+            const uint32_t type = __float_as_uint(q1.w) & 15u;
+            if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                const f3 oc = sub(o, xyz(q0));
+                const float b = dot(oc, d);
+                const float c = dot(oc, oc) - q1.x;
+                const float disc = b * b - a_dd * c;
+                if (disc > 0) {
+                    float t = (-b - sqrtf(disc)) / a_dd;
+                    if (!(t < t_best && t > kTmin)) t = (-b + sqrtf(disc)) / a_dd;
+                    if (t < t_best && t > kTmin) {
+                        t_best = t;
+                        hit = i;
+                        tag = __float_as_uint(q1.w);
+                    }
+                }
+            } else {  // XY/XZ/YZRect::Hit
+                const float ok = type == RT_XYRECT ? o.z : (type == RT_XZRECT ? o.y : o.x);
+                const float ik = type == RT_XYRECT ? inv.z : (type == RT_XZRECT ? inv.y : inv.x);
+                const float t = (q0.x - ok) * ik;
+                if (!(t < kTmin || t > t_best)) {
+                    const float oa = type == RT_YZRECT ? o.y : o.x, da = type == RT_YZRECT ? d.y : d.x;
+                    const float ob = type == RT_XYRECT ? o.y : o.z, db = type == RT_XYRECT ? d.y : d.z;
+                    const float xx = oa + t * da;
+                    const float yy = ob + t * db;
+                    if (!(xx < q0.y || xx > q0.z || yy < q0.w || yy > q1.x)) {
+                        t_best = t;
+                        hit = i;
+                        tag = __float_as_uint(q1.w);
+                    }
+                }
+            }
+        }
+    }
+    return HitOut{hit, tag, t_best};
+}
+
+// Reference exactness of the BVH kernels (v1-v4).  Their SAH tree, on padded boxes with conservative culling, returns
+// the geometric closest hit p* at t*: every primitive whose test accepts the ray is tested.  The reference's
+// BVHNode::Hit (Hittable.cuh:387-439) returns the same unless (a) a box on p*'s path rejects the ray, (b) another
+// primitive ties at t* (which one it keeps depends on its culling and order), or (c) a NaN took part.
+//   (a) The boxes on p*'s path contain p*'s own reference box as floats (SurroundingBox is fmin / fmax), each is tested
+//   against the closest hit as of its push, which is >= t*, and AABB::Hit's arithmetic — (bound - o) · (1/d), then
+//   max / min — is monotone in the bound and in t_max (round-to-nearest is).  So if AABB::Hit(p*'s own box, 0.001, t*)
+//   accepts the ray with the reference's own arithmetic, every box on the path accepts it too; only rays it rejects —
+//   a ray grazing an edge or corner of that box, a hit within rounding of the box face it enters by — can differ.
+//   (b) is tracked by the leaf tests: a candidate equal to the closest hit so far sets kTieBit in the hit index, a
+//   strictly closer hit clears it.  (c): a slab distance or a rectangle's t is NaN only as 0 · inf, so only on a ray
+//   with a direction component outside [2^-40, 2^40] in magnitude (zero included) or a non-finite origin; such a ray
+//   replays whatever it hit (the reference may test a rectangle whose own box the SAH tree culls).
+// Checked by shade() (EXACT) on the hit record it loads anyway, in two stages.  Stage 1, per ray: the hit point
+// p = o + t*·d (the hit record's own expression) lies inside p*'s own box by a margin of 2^-20 · S, S = Σ_a (|o_a| +
+// |t*·d_a|), on every axis — AABB::Hit's computed slab distances are within ~3 ulps of the true ones and p within ~2 ulps
+// of o + t*·d, so the margin leaves a factor > 4 and AABB::Hit accepts.  A sphere's test reads |p - c| < r - 2^-19 (S +
+// r) per axis from the hit record's own p - c (its box is c -/+ r; the extra terms cover the rounding of p - c and of
+// c -/+ r); a rectangle's in-plane axes compare p with its extents; in its plane axis, where p lies on k inside the
+// box's k -/+ 0.0001, the slab distances are computed exactly as AABB::Hit does, (k -/+ 0.0001 - o) · RN(1/d), and
+// compared with t* = (k - o) · RN(1/d), the rectangle test's own expression.  Stage 2, for the rays stage 1 does not
+// clear (a hit near a face of its box, or coordinates too large for the margin): AABB::Hit itself on the box
+// (bvh_boxes).  A ray neither clears — a rejected own box, a tie, (c) — makes shade() return SHADE_REPLAY with its
+// path state untouched; the kernel replays the reference BVH for it (ref_trace over bvh_ref_nodes, whose leaves index
+// the BVH-order records, at a point of its loop where few registers are live: bvh_replay) and shades the answer, marked
+// kVerifiedBit (a verified miss: kVerifiedMiss), without a second check.
+constexpr int kVerifiedBit = 0x20000000;  // in a hit index: the reference traversal's own answer (bvh_replay)
+constexpr int kVerifiedMiss = -2;
+__device__ __forceinline__ bool bvh_odd_ray(const f3 ro, const f3 rd) {
+    // (c): a direction component outside [2^-40, 2^40] in magnitude (zero, NaN and inf included: NaN fails every
+    // comparison and propagates through the sum) or a non-finite origin
+    const float ax = fabsf(rd.x), ay = fabsf(rd.y), az = fabsf(rd.z);
+    const float lo = fminf(fminf(ax, ay), az), hi = fmaxf(fmaxf(ax, ay), az);
+    const float so = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z);
+    return !(lo >= 0x1p-40f && hi <= 0x1p40f && ax + ay + az == ax + ay + az && so <= FLT_MAX);
+}
+// Whether (hit, t) is the reference's answer for the ray (see above); strips kTieBit / kVerifiedBit from `hit`.
+// q = p - c of a sphere hit (its normal's numerator).  (c) is tested only where it can matter: stage 1 of a sphere hit
+// needs no finite 1/d (a zero or tiny component leaves its axis unconstrained in AABB::Hit: an infinite slab; NaNs fail
+// its comparisons), a rectangle hit needs its plane axis' RN(1/d) to be rcp_rn's, stage 2 needs every axis'; and a
+// miss can be a NaN hit of the reference's only in a scene with rectangles.
+template <class PP>
+__device__ __forceinline__ bool bvh_clear(PP P, int& hit, const uint32_t tag, const float t, const f3 ro, const f3 rd,
+                                          const float4 p0, const float4 p1, const f3 td, const f3 p, const f3 q) {
+    const bool miss = hit < 0;
+    const bool tie = !miss && (hit & kTieBit) != 0;
+    const bool verified = miss ? hit == kVerifiedMiss : (hit & kVerifiedBit) != 0;
+    hit = miss ? -1 : (hit & (kVerifiedBit - 1));
+    if (RT_BVH_EXACT == 0 || RT_BVH_EXACT == 3 || verified || P->bvh_ref_nodes == nullptr) return true;
+    bool clear;
+    if (miss) {
+        clear = !(P->bvh_has_rects && bvh_odd_ray(ro, rd));
+    } else {
+        clear = !tie && t > kTmin;  // (a rectangle accepts t* = 0.001, which AABB::Hit's t_min rejects)
+        const float S = (fabsf(ro.x) + fabsf(td.x)) + (fabsf(ro.y) + fabsf(td.y)) + (fabsf(ro.z) + fabsf(td.z));
+        const uint32_t type = tag & 15u;
+        if (type == RT_SPHERE) {  // own box: centre -/+ radius (Hittable.cuh:112-116)
+            const float r = p0.w;
+            const float R = __builtin_fmaf(S, -0x1p-19f, r * (1.0f - 0x1p-19f));
+            clear = clear && fabsf(q.x) < R && fabsf(q.y) < R && fabsf(q.z) < R;
+        } else {  // own box: the extents, and k -/+ 0.0001 in the plane axis (Hittable.cuh:171-181, 227-237, 283-293)
+            const float m = __builtin_fmaf(S, 0x1p-20f, 0x1p-100f);
+            const bool yz = type == RT_YZRECT, xy = type == RT_XYRECT, xz = type == RT_XZRECT;
+            const float pa = yz ? p.y : p.x, pb = xy ? p.y : p.z;
+            const float dk = xy ? rd.z : (xz ? rd.y : rd.x);
+            const float ok = xy ? ro.z : (xz ? ro.y : ro.x), ik = rcp_rn(dk);
+            const float s0 = (p0.x - 0.0001f - ok) * ik, s1 = (p0.x + 0.0001f - ok) * ik;
+            const bool neg = ik < 0.0f;
+            clear = clear && in_rcp_range(dk) && (pa - p0.y) > m && (p0.z - pa) > m && (pb - p0.w) > m &&
+                    (p1.x - pb) > m && (neg ? s1 : s0) < t && (neg ? s0 : s1) > t;
+        }
+        if (!clear && !tie && t > kTmin && !bvh_odd_ray(ro, rd)) {
+            // stage 2 (rare): AABB::Hit(own box, 0.001, t*) with the reference's arithmetic
+            const float4* boxes = P->bvh_boxes;
+            clear = ref_box(boxes[2 * hit], boxes[2 * hit + 1], ro, mk(rcp_rn(rd.x), rcp_rn(rd.y), rcp_rn(rd.z)), t);
+        }
+    }
+    if (RT_BVH_EXACT == 2) {  // (A/B builds: the check without the replay)
+        asm volatile("" ::"v"((uint32_t)clear));
+        return true;
+    }
+    return clear;
+}
+// The reference traversal's answer for a ray shade() returned SHADE_REPLAY for, marked verified.
+template <class PP>
+__device__ __noinline__ void bvh_replay(PP P, const float4* __restrict__ prims, int& hit, uint32_t& tag, float& t,
+                                        const f3 ro, const f3 rd) {
+    if (RT_BVH_EXACT == 4) {  // (A/B builds: the replay's call without the reference traversal — wrong images)
+        hit = hit >= 0 ? (hit | kVerifiedBit) : kVerifiedMiss;
+        return;
+    }
+    const HitOut r = ref_trace<kRefStackBvh>(P->bvh_ref_nodes, prims, ro, rd);
+    hit = r.hit >= 0 ? (r.hit | kVerifiedBit) : kVerifiedMiss;
+    tag = r.tag;
+    t = r.t;
+}
+
+// The reference traversal (ref_trace's algorithm and arithmetic) for one wave-uniform ray, without a call or private
+// memory: every value is uniform — node and primitive records are scalar loads, the tests' arithmetic runs on uniform
+// operands — and the stack lives across the lanes of two VGPRs (entry j in lane j, v_writelane / v_readlane at the
+// uniform top; at most kRefTreeMaxDepthBvh + 1 < 64 entries).  Every lane of the wave must be active (v3 and v4 keep
+// all 64 lanes in their loops), so no copy of the stack registers can drop a lane.
+typedef const __attribute__((address_space(4))) float ConstF32R;
+__device__ __forceinline__ uint32_t lane_write(uint32_t vec, const uint32_t val, const uint32_t lane) {
+    // (gfx9 reads one SGPR per VALU instruction: the lane select goes through M0)
+    const uint32_t v = __builtin_amdgcn_readfirstlane(val), l = __builtin_amdgcn_readfirstlane(lane);
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(vec) : "s"(v), "{m0}"(l));
+    return vec;
+}
+__device__ __forceinline__ HitOut ref_trace_wave(const float4* __restrict__ rnodes, const float4* __restrict__ prims,
+                                                 const f3 o, const f3 d) {
+    int hit = -1;
+    uint32_t tag = 0u;
+    float t_best = FLT_MAX;
+    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float a_dd = dot(d, d);
+    const auto rec = [](const float4* base, const uint32_t i, float4& a, float4& b) {  // 32-B record i, scalar loads
+        const ConstF32R* q = (const ConstF32R*)base + 8u * i;
+        a = make_float4(q[0], q[1], q[2], q[3]);
+        b = make_float4(q[4], q[5], q[6], q[7]);
+    };
+    float4 lo, hi;
+    rec(rnodes, 0u, lo, hi);
+    if (!ref_box(lo, hi, o, inv, FLT_MAX)) return HitOut{hit, tag, t_best};  // its own box first (Hittable.cuh:389)
+    uint32_t stk_n = 0u, stk_t = __float_as_uint(FLT_MAX);  // lane 0: the root, pushed with t_max = FLT_MAX
+    int top = 0;
+    while (top >= 0) {
+        const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)stk_n, top);
+        const float tm = __int_as_float(__builtin_amdgcn_readlane((int)stk_t, top));
+        top--;
+        rec(rnodes, n, lo, hi);
+        if (!ref_box(lo, hi, o, inv, tm)) continue;
+        const int ch[2] = {__float_as_int(lo.w), __float_as_int(hi.w)};
+        for (int k = 0; k < 2; k++) {
+            if (ch[k] >= 0) {
+                top++;
+                stk_n = lane_write(stk_n, (uint32_t)ch[k], (uint32_t)top);
+                stk_t = lane_write(stk_t, __float_as_uint(t_best), (uint32_t)top);
+                continue;
+            }
+            const uint32_t i = (uint32_t)~ch[k];  // PerformHit (Hittable.cuh:470-485) with t_max = the closest hit so far
+            float4 q0, q1;
+            rec(prims, i, q0, q1);
+            const uint32_t type = __float_as_uint(q1.w) & 15u;
+            if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
+                const f3 oc = sub(o, xyz(q0));
+                const float b = dot(oc, d);
+                const float c = dot(oc, oc) - q1.x;
+                const float disc = b * b - a_dd * c;
+                if (disc > 0) {
+                    float t = (-b - sqrtf(disc)) / a_dd;
+                    if (!(t < t_best && t > kTmin)) t = (-b + sqrtf(disc)) / a_dd;
+                    if (t < t_best && t > kTmin) {
+                        t_best = t;
+                        hit = (int)i;
+                        tag = __float_as_uint(q1.w);
+                    }
+                }
+            } else {  // XY/XZ/YZRect::Hit
+                const float ok = type == RT_XYRECT ? o.z : (type == RT_XZRECT ? o.y : o.x);
+                const float ik = type == RT_XYRECT ? inv.z : (type == RT_XZRECT ? inv.y : inv.x);
+                const float t = (q0.x - ok) * ik;
+                if (!(t < kTmin || t > t_best)) {
+                    const float oa = type == RT_YZRECT ? o.y : o.x, da = type == RT_YZRECT ? d.y : d.x;
+                    const float ob = type == RT_XYRECT ? o.y : o.z, db = type == RT_XYRECT ? d.y : d.z;
+                    const float xx = oa + t * da;
+                    const float yy = ob + t * db;
+                    if (!(xx < q0.y || xx > q0.z || yy < q0.w || yy > q1.x)) {
+                        t_best = t;
+                        hit = (int)i;
+                        tag = __float_as_uint(q1.w);
+                    }
+                }
+            }
+        }
+    }
+    return HitOut{hit, tag, t_best};
+}
 // acos / atan2 of GetSphereUV (Hittable.cuh:119-125) as fixed sequences of binary32 +, -, *, / and sqrt
 // (Cephes asinf/atanf polynomials, ~2 ulp), identical operation for operation in oracle/rt_oracle.c.  The
 // reference's CUDA acos/atan2 under -use_fast_math cannot be reproduced, and the device library's and
@@ -491,8 +780,11 @@ __device__ __forceinline__ TexFetch texture_fetch(const float4& m0, const float4
     }
     return f;
 }
+// An RGB8 texel's dword is not 4-byte aligned: loaded through an alignment-1 type (one global_load_dword on gfx950,
+// whose vector memory accesses need no alignment)
+typedef uint32_t UnalignedU32 __attribute__((aligned(1)));
 __device__ __forceinline__ uint32_t texture_gather(const TexFetch& f, const void* dummy) {
-    return *reinterpret_cast<const uint32_t*>(f.pending ? f.texel : reinterpret_cast<const uint8_t*>(dummy));
+    return *reinterpret_cast<const UnalignedU32*>(f.pending ? f.texel : reinterpret_cast<const uint8_t*>(dummy));
 }
 __device__ __forceinline__ f3 texture_resolve(const TexFetch& f, uint32_t w) {
     if (!f.pending) return f.color;
@@ -504,7 +796,7 @@ __device__ __forceinline__ f3 texture_value(const float4& m0, const float4& m1, 
                                             float u, float v, f3 p, const int4* __restrict__ imgs,
                                             const uint8_t* __restrict__ texels) {
     const TexFetch f = texture_fetch(m0, m1, m2, tex_type, u, v, p, imgs, texels);
-    return f.pending ? texture_resolve(f, *reinterpret_cast<const uint32_t*>(f.texel)) : f.color;
+    return f.pending ? texture_resolve(f, *reinterpret_cast<const UnalignedU32*>(f.texel)) : f.color;
 }
 
 __device__ __forceinline__ uint32_t f2u8(float f) { return f != f ? 0u : (uint32_t)(int)f; }
@@ -551,16 +843,28 @@ __device__ __forceinline__ void camera_ray(PP P, const Camera& cam, R& rng, f3& 
 // DEFER (flat kernels): RandomInUnitSphere makes at most P->rius_cap attempts; SHADE_DEFERRED when all were rejected — ro, rd
 // and att are untouched, and the lane shades the same hit again at the next pass, continuing the same call.
 enum ShadeResult { SHADE_CONTINUE = 0, SHADE_ENDED = 1, SHADE_DEFERRED = 2 };
-template <bool TEX = true, bool DEFER = false, class PP, class R>
+// EXACT (the BVH kernels): `hit` may carry kTieBit / kVerifiedBit; SHADE_REPLAY when the closest hit may not be the
+// reference's (bvh_clear) — nothing is changed, and the kernel replays the reference traversal (bvh_replay).
+enum { SHADE_REPLAY = 3 };
+template <bool TEX = true, bool DEFER = false, bool EXACT = false, class PP, class R>
 __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, const float4* __restrict__ mats,
                                      const int4* __restrict__ imgs, int hit, uint32_t hit_tag, float t,
                                      f3& ro, f3& rd, f3& att, R& rng, bool rtl, f3& contrib) {
+    float4 p0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), p1 = p0;
     // unit_vector(rd) is needed by the sky (y only), Metal and Dielectric: computed once for all lanes of
     // the wave that need it instead of once per material branch (same binary32 operations, Math.cuh:210-213)
     // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
-    // primitive — the material load need not wait for the primitive's
+    // primitive — the material load need not wait for the primitive's (nor for the exactness check)
     uint32_t mtype = 0xffu;  // 0xff: miss
     if (hit >= 0) mtype = __float_as_uint(mats[3 * (hit_tag >> 4)].x) & 15u;
+    if constexpr (EXACT) {
+        const int h = hit >= 0 ? (hit & (kVerifiedBit - 1)) : 0;
+        p0 = prims[2 * h + 0];  // (the record of primitive 0 for a miss: read, never used)
+        p1 = prims[2 * h + 1];
+        const f3 td = scale(t, rd);  // (the hit point and p - c: shared with the hit record below)
+        const f3 ph = add(ro, td);
+        if (!bvh_clear(P, hit, hit_tag, t, ro, rd, p0, p1, td, ph, sub(ph, xyz(p0)))) return SHADE_REPLAY;
+    }
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
     if (hit < 0) {  // sky (Kernel.cu:41-44)
         // rd.y / |rd|: below |rd.y| = 2^-100 the quotient's exact bits vanish in the + 1 (|q| < 2^-60)
@@ -573,8 +877,10 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, con
         contrib = mulv(att, c);
         return SHADE_ENDED;
     }
-    const float4 p0 = prims[2 * hit + 0];
-    const float4 p1 = prims[2 * hit + 1];
+    if constexpr (!EXACT) {
+        p0 = prims[2 * hit + 0];
+        p1 = prims[2 * hit + 1];
+    }
     const uint32_t type = hit_tag & 15u, mat = hit_tag >> 4;
     const float4 m0 = mats[3 * mat + 0];
     const uint32_t ttype = (__float_as_uint(m0.x) >> 4) & 15u;
@@ -750,6 +1056,7 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cnt
             atomicAdd(&P.counters[14], (unsigned long long)cnt.idle_fin);
             atomicAdd(&P.counters[15], (unsigned long long)cnt.idle_wait);
             atomicAdd(&P.counters[16], (unsigned long long)cnt.rects);
+            atomicAdd(&P.counters[17], (unsigned long long)cnt.replays);
             if (cnt.ctotal && wave_leader()) {  // one lane per wave: the stamps are wave-uniform
                 atomicAdd(&P.counters[7], (unsigned long long)cnt.ctrav);
                 atomicAdd(&P.counters[8], (unsigned long long)cnt.cshade);
@@ -1041,9 +1348,16 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
                 cnt.rays++;
                 const float a_dd = dot(rd, rd);
                 float t;
-                const int hit = trace<COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, cnt);
+                int hit = trace<COUNT_TESTS>(nodes, prims, P.num_nodes, ro, rd, a_dd, t, cnt);
                 if (COUNT_TESTS) cnt.wshade += wave_leader();
-                done = shade(&P, prims, P.mats, P.imgs, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
+                uint32_t tag = hit >= 0 ? __float_as_uint(prims[2 * (hit & (kTieBit - 1)) + 1].w) : 0u;
+                int res = shade<true, false, true>(&P, prims, P.mats, P.imgs, hit, tag, t, ro, rd, att, rng, rtl, contrib);
+                if (res == SHADE_REPLAY) {  // (bvh_clear)
+                    if (COUNT_TESTS) cnt.replays++;
+                    bvh_replay(&P, prims, hit, tag, t, ro, rd);
+                    res = shade<true, false, true>(&P, prims, P.mats, P.imgs, hit, tag, t, ro, rd, att, rng, rtl, contrib);
+                }
+                done = res == SHADE_ENDED;
                 if (!done) depth++;
             }
             if (done) {
@@ -1070,6 +1384,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const KParams P) {
 constexpr int kSentinel = 0x7fffffff;  // traversal finished (internal node ids are < it, leaves < 0)
 enum LaneMode { MODE_TRAV = 0, MODE_SHADE = 1, MODE_DONE = 2 };
 constexpr int MODE_NEED = 3;  // v4 / persistent flat: the lane waits for a pixel; v3 sample items: for a sample
+constexpr int MODE_REPLAY = 4;  // v3 / v4: the closest hit replays the reference traversal before shading (bvh_replay)
 
 template <bool COUNT_TESTS, int BLOCK = 64>
 __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
@@ -1207,10 +1522,13 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
                                     t_best = t;
                                     hit = (int)i;
                                 } else {
+                                    const bool tied = t == t_best;  // (bvh_clear)
                                     t = (-b + sq) / a_dd;
                                     if (t < t_best && t > kTmin) {
                                         t_best = t;
                                         hit = (int)i;
+                                    } else if (tied || t == t_best) {
+                                        hit |= kTieBit;
                                     }
                                 }
                             }
@@ -1224,8 +1542,8 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
                                 const float xx = oa + t * da;
                                 const float yy = ob + t * db;
                                 if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
+                                    hit = t == t_best ? (int)i | kTieBit : (int)i;
                                     t_best = t;
-                                    hit = (int)i;
                                 }
                             }
                         }
@@ -1243,7 +1561,14 @@ __global__ __launch_bounds__(BLOCK) void render_kernel_v2(const KParams P) {
         if (mode == MODE_SHADE) {
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
-            if (shade(&P, prims, P.mats, P.imgs, hit, hit >= 0 ? __float_as_uint(prims[2 * hit + 1].w) : 0u, t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED) {
+            uint32_t tag = hit >= 0 ? __float_as_uint(prims[2 * (hit & (kTieBit - 1)) + 1].w) : 0u;
+            int res = shade<true, false, true>(&P, prims, P.mats, P.imgs, hit, tag, t_best, ro, rd, att, rng, rtl, contrib);
+            if (res == SHADE_REPLAY) {  // (bvh_clear)
+                if (COUNT_TESTS) cnt.replays++;
+                bvh_replay(&P, prims, hit, tag, t_best, ro, rd);
+                res = shade<true, false, true>(&P, prims, P.mats, P.imgs, hit, tag, t_best, ro, rd, att, rng, rtl, contrib);
+            }
+            if (res == SHADE_ENDED) {
                 next_sample(contrib);
             } else if (++depth >= P.max_depth) {
                 next_sample(mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
@@ -1296,6 +1621,30 @@ struct Cursor {
     int mode;
 };
 
+// v3 / v4: the lanes in MODE_REPLAY (shade() returned SHADE_REPLAY), one after another, through ref_trace_wave; each
+// gets the reference traversal's answer, marked verified, and goes to MODE_SHADE.  Called where every lane is active.
+template <class PP>
+__device__ __forceinline__ void bvh_replay_wave(PP P, const float4* __restrict__ prims, Cursor& c, const f3 ro, const f3 rd,
+                                                Counts& cnt, const bool count) {
+    uint64_t need = __ballot(c.mode == MODE_REPLAY);
+    while (need != 0u) {
+        const int L = (int)__builtin_ctzll(need);
+        need &= need - 1u;
+        const auto bl = [L](const float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L)); };
+        const HitOut r = ref_trace_wave(P->bvh_ref_nodes, prims, mk(bl(ro.x), bl(ro.y), bl(ro.z)), mk(bl(rd.x), bl(rd.y), bl(rd.z)));
+        if (__lane_id() == (uint32_t)L) {
+            c.hit = RT_BVH_EXACT == 4 ? (c.hit >= 0 ? (c.hit | kVerifiedBit) : kVerifiedMiss)  // (A/B: no replay)
+                                      : (r.hit >= 0 ? (r.hit | kVerifiedBit) : kVerifiedMiss);
+            if (RT_BVH_EXACT != 4) {
+                c.tag = r.tag;
+                c.t_best = r.t;
+            }
+            c.mode = MODE_SHADE;
+            if (count) cnt.replays++;
+        }
+    }
+}
+
 template <bool WIDE>
 __device__ __forceinline__ void v3_start_trace(uint32_t num_nodes, Cursor& c, uint32_t& rays) {
     rays++;
@@ -1313,14 +1662,14 @@ __device__ __forceinline__ void v3_next_sample(const KParams& P, uint32_t x, uin
                                                f3& col, f3& att, uint32_t& sample, uint32_t& depth, f3& ro,
                                                f3& rd, Cursor& c, uint32_t& rays) {
     col = add_sample(rng, col, contrib);
-    KParamsC* q = kparams_reload();
+    KParamsC* q = kparams_reload();  // (launch-uniform operands re-read here, not held in SGPRs through the loop)
     const Camera cam = lane_camera(q, x, g);
-    while (++sample < P.spp) {
+    while (++sample < q->spp) {
         camera_ray(q, cam, rng, ro, rd, sample);
         att = mk(1.0f, 1.0f, 1.0f);
         depth = 0;
-        if (P.max_depth > 0) {
-            v3_start_trace<WIDE>(P.num_nodes, c, rays);
+        if (q->max_depth > 0) {
+            v3_start_trace<WIDE>(q->num_nodes, c, rays);
             return;
         }
         col = add_sample(rng, col, mk(0.0f, 0.0f, 0.0f));  // exceeded recursion (Kernel.cu:79)
@@ -1413,7 +1762,7 @@ constexpr uint32_t kPrimStep = 32u;  // leaf cursor unit: bytes of one 32-B prim
 // Traversal phase of one lane (v3/v4): resumes the cursor and runs the speculative while-while loop
 // until this lane's closest hit is found (mode -> MODE_SHADE) or fewer than `threshold` lanes are
 // still tracing (the wave then shades the finished lanes and regenerates them).
-template <bool COUNT_TESTS, int NODES, uint32_t STK_OFF, bool WIDE>
+template <bool COUNT_TESTS, int NODES, uint32_t STK_OFF, bool WIDE, bool EXACT = RT_BVH_EXACT != 0>
 __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
                                             const float4* __restrict__ nodes_tab, const uint32_t* __restrict__ refs,
                                             const float4* __restrict__ prims, typename RefW<WIDE>::Entry* const stk,
@@ -1647,11 +1996,14 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
                             hit = (int)i;
                             tag = __float_as_uint(p1.w);
                         } else {
+                            const bool tied = EXACT && t == t_best;  // (bvh_clear: a tie at the closest hit so far)
                             t = fast_div ? div_rn(-b + sq, a_dd, inv_a) : (-b + sq) / a_dd;
                             if (t < t_best && t > kTmin) {
                                 t_best = t;
                                 hit = (int)i;
-                            tag = __float_as_uint(p1.w);
+                                tag = __float_as_uint(p1.w);
+                            } else if (EXACT && (tied || t == t_best)) {
+                                hit |= kTieBit;
                             }
                         }
                     }
@@ -1665,8 +2017,8 @@ __device__ __forceinline__ void v3_traverse(const __amdgpu_buffer_rsrc_t nrsrc,
                         const float xx = oa + t * da;
                         const float yy = ob + t * db;
                         if (!(xx < p0.y || xx > p0.z || yy < p0.w || yy > p1.x)) {
+                            hit = EXACT && t == t_best ? (int)i | kTieBit : (int)i;  // (a rectangle re-accepts an equal t)
                             t_best = t;
-                            hit = (int)i;
                             tag = __float_as_uint(p1.w);
                         }
                     }
@@ -1733,7 +2085,10 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     size_t pix;
     const uint32_t slot = blockIdx.x;
     const uint32_t tile = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
-    if (!lane_pixel<64>(P, x, g, pix, tile)) return;
+    // a lane outside the image (a partial tile) stays in the loop as a finished lane: the wave's reference replay
+    // (bvh_replay_wave) keeps its stack across all 64 lanes
+    const bool live = lane_pixel<64>(P, x, g, pix, tile);
+    if (!live) x = g = 0u, pix = 0u;  // (renders pixel 0's first camera ray, then leaves it: nothing is written)
     const bool rtl = P.rius_rtl != 0;
     stk[0] = (Entry)RefW<WIDE>::kSentinel;   // two sentinel pads below the stack: popping an empty stack
     stk[64] = (Entry)RefW<WIDE>::kSentinel;  // yields the sentinel without a bounds test
@@ -1751,7 +2106,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     // (words 0, 5) and this mode's parking (no colour words) leave free; word 8 counts the lane's finished paths' rays
     // (the packed 13-bit ray field holds one path's); the packed sample field holds the item's pixel.
     constexpr bool kItemsBuild = PHILOX && COMPACT;
-    const bool items = kItemsBuild && P.spp > 0 && P.max_depth > 0 && __ballot(1) == ~0ull;  // (wave-uniform)
+    const bool items = kItemsBuild && P.spp > 0 && P.max_depth > 0 && __ballot(live) == ~0ull;  // (wave-uniform)
     uint32_t next_item = 64u;  // wave-uniform: items 0-63 (every pixel's sample 0) start below
     const uint32_t n_items = P.spp * 64u;
     const auto item_sum = [&](uint32_t p, int ch) -> unsigned long long* {
@@ -1771,12 +2126,15 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             park[6 * 64] = park[7 * 64] = park[8 * 64] = 0u;
         }
     }
+    if (!live) c.mode = MODE_DONE;
     const uint32_t threshold = P.regen_threshold;
 
     const uint64_t t_start = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t w_start = __builtin_amdgcn_s_memtime();
     while (true) {
+        // shade() returned SHADE_REPLAY for these lanes: the path state is parked, few registers are live
+        if (__ballot(c.mode == MODE_REPLAY) != 0u) bvh_replay_wave(kparams_reload(), prims, c, ro, rd, cnt, COUNT_TESTS);
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
         if (c.mode == MODE_TRAV) {
@@ -1795,12 +2153,16 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
             KParamsC* const q = kparams_reload();
-            bool ended = shade<TEX>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
-            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+            const int res = shade<TEX, false, true>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng,
+                                                    rtl, contrib);
+            bool ended = res == SHADE_ENDED;
+            if (res != SHADE_REPLAY && !ended && ++depth >= q->max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
-            if (kItemsBuild && items && ended) {  // this sample into its pixel's sums; the lane takes the next item below
+            if (res == SHADE_REPLAY) {  // (nothing changed: re-parked as it was, replayed at the loop's top)
+                c.mode = MODE_REPLAY;
+            } else if (kItemsBuild && items && ended) {  // this sample into its pixel's sums; the lane takes the next item below
                 const uint32_t q0 = quant12(contrib.x), q1 = quant12(contrib.y), q2 = quant12(contrib.z);
                 if (q0) atomicAdd(item_sum(sample, 0), (unsigned long long)q0);
                 if (q1) atomicAdd(item_sum(sample, 1), (unsigned long long)q1);
@@ -1857,6 +2219,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         const uint64_t c = (__builtin_amdgcn_s_memtime() - w_start) >> 8;
         P.tile_cost[tile] = c > 0xffffffffull ? 0xffffffffu : (uint32_t)c;
     }
+    if (!live) return;
     R rng;
     f3 col, att;
     uint32_t sample, depth, rays;
@@ -1907,7 +2270,7 @@ __global__ __launch_bounds__(64, 8) void trace_rays_kernel(const KParams P, cons
         if (c.mode == MODE_TRAV) {
             uint32_t thr = P.regen_threshold;
             if (P.regen_live_frac) thr = min(thr, ((uint32_t)__popcll(__ballot(c.mode != MODE_DONE)) * P.regen_live_frac) >> 6);
-            v3_traverse<COUNT_TESTS, NODES_48, 0u, false>(nrsrc, P.nodes48, P.refs, P.prims, stk, thr, ro, rd, c, cnt, 64u,
+            v3_traverse<COUNT_TESTS, NODES_48, 0u, false, false>(nrsrc, P.nodes48, P.refs, P.prims, stk, thr, ro, rd, c, cnt, 64u,
                                                            P.leaf_break);
         }
         if (c.mode == MODE_SHADE) {
@@ -2143,6 +2506,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     const uint64_t rt_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0u;
 
     while (true) {
+        // shade() returned SHADE_REPLAY for these lanes: the path state is parked, few registers are live
+        if (__ballot(c.mode == MODE_REPLAY) != 0u) bvh_replay_wave(kparams_reload(), prims, c, ro, rd, cnt, COUNT_TESTS);
         if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
@@ -2154,12 +2519,16 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
             f3 contrib;
             if (COUNT_TESTS) cnt.wshade += wave_leader();
             KParamsC* const q = kparams_reload();
-            bool ended = shade<TEX>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng, rtl, contrib) == SHADE_ENDED;
-            if (!ended && ++depth >= P.max_depth) {  // exceeded recursion (Kernel.cu:79)
+            const int res = shade<TEX, false, true>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng,
+                                                    rtl, contrib);
+            bool ended = res == SHADE_ENDED;
+            if (res != SHADE_REPLAY && !ended && ++depth >= q->max_depth) {  // exceeded recursion (Kernel.cu:79)
                 ended = true;
                 contrib = mk(0.0f, 0.0f, 0.0f);
             }
-            if (ended) {
+            if (res == SHADE_REPLAY) {  // (nothing changed: re-parked as it was, replayed at the loop's top)
+                c.mode = MODE_REPLAY;
+            } else if (ended) {
                 col = add_sample(rng, col, contrib);  // Kernel.cu:147
                 if (++sample < P.spp) {
                     cam = true;
@@ -2218,101 +2587,6 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
 // skips that pass's trace, instead of every lane of the wave waiting for the wave's slowest sampler.  Per lane the
 // rays, RNG draws and arithmetic are those of the other kernels (tests/test_gpu_parity.py runs it on every case).
 // ---------------------------------------------------------------------------------------------------
-// The reference's own closest-hit query, replayed exactly: BVHNode::Hit (Hittable.cuh:387-439) over the tree the
-// BVHNode constructor builds (ref_nodes, scene_build.cpp), with AABB::Hit (AABB.cuh:30-50) on the reference's boxes and
-// its t_max bookkeeping (a node's box is tested against the closest hit as of its push).  Per lane, with a private
-// stack: the flat kernel runs it only for the rare rays whose answer box culling could change (flat_trace).
-constexpr int kRefStack = 16;  // > kRefTreeMaxDepth (rt_internal.h)
-__device__ __forceinline__ bool ref_box(const float4 lo, const float4 hi, const f3 o, const f3 inv, float t_max) {
-    float t_min = kTmin;
-    const float los[3] = {lo.x, lo.y, lo.z}, his[3] = {hi.x, hi.y, hi.z};
-    const float os[3] = {o.x, o.y, o.z}, invs[3] = {inv.x, inv.y, inv.z};
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        float t0 = (los[a] - os[a]) * invs[a];
-        float t1 = (his[a] - os[a]) * invs[a];
-        if (invs[a] < 0.0f) {
-            const float tmp = t0;
-            t0 = t1;
-            t1 = tmp;
-        }
-        t_min = t0 > t_min ? t0 : t_min;
-        t_max = t1 < t_max ? t1 : t_max;
-        if (t_max <= t_min) return false;
-    }
-    return true;
-}
-struct HitOut {
-    int hit;
-    uint32_t tag;
-    float t;
-};
-// (not inlined: the flat kernels' registers are sized for their common path; the result comes back in registers)
-__device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, const float4* __restrict__ prims, const f3 o,
-                                         const f3 d) {
-    int hit = -1;
-    uint32_t tag = 0u;
-    float t_best = FLT_MAX;  // = rec.t once something is hit (the reference's "hit_something ? rec.t : t_max")
-    const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float a_dd = dot(d, d);
-    int stk[kRefStack];
-    float stm[kRefStack];
-    if (!ref_box(rnodes[0], rnodes[1], o, inv, FLT_MAX)) return HitOut{hit, tag, t_best};  // its own box first (:389)
-    int top = 0;
-    stk[0] = 0;
-    stm[0] = FLT_MAX;
-    while (top >= 0) {
-        const int n = stk[top];
-        const float tm = stm[top];
-        top--;
-        const float4 lo = rnodes[2 * n], hi = rnodes[2 * n + 1];
-        if (!ref_box(lo, hi, o, inv, tm)) continue;
-        const int ch[2] = {__float_as_int(lo.w), __float_as_int(hi.w)};
-        for (int k = 0; k < 2; k++) {
-            if (ch[k] >= 0) {
-                top++;
-                stk[top] = ch[k];
-                stm[top] = t_best;
-                continue;
-            }
-            const int i = ~ch[k];  // PerformHit (Hittable.cuh:470-485) with t_max = the closest hit so far
-            const float4 q0 = prims[2 * i], q1 = prims[2 * i + 1];
-            const uint32_t type = __float_as_uint(q1.w) & 15u;
-            if (type == RT_SPHERE) {  // Sphere::Hit (Hittable.cuh:80-110)
-                const f3 oc = sub(o, xyz(q0));
-                const float b = dot(oc, d);
-                const float c = dot(oc, oc) - q1.x;
-                const float disc = b * b - a_dd * c;
-                if (disc > 0) {
-                    float t = (-b - sqrtf(disc)) / a_dd;
-                    if (!(t < t_best && t > kTmin)) t = (-b + sqrtf(disc)) / a_dd;
-                    if (t < t_best && t > kTmin) {
-                        t_best = t;
-                        hit = i;
-                        tag = __float_as_uint(q1.w);
-                    }
-                }
-            } else {  // XY/XZ/YZRect::Hit
-                const float ok = type == RT_XYRECT ? o.z : (type == RT_XZRECT ? o.y : o.x);
-                const float ik = type == RT_XYRECT ? inv.z : (type == RT_XZRECT ? inv.y : inv.x);
-                const float t = (q0.x - ok) * ik;
-                if (!(t < kTmin || t > t_best)) {
-                    const float oa = type == RT_YZRECT ? o.y : o.x, da = type == RT_YZRECT ? d.y : d.x;
-                    const float ob = type == RT_XYRECT ? o.y : o.z, db = type == RT_XYRECT ? d.y : d.z;
-                    const float xx = oa + t * da;
-                    const float yy = ob + t * db;
-                    if (!(xx < q0.y || xx > q0.z || yy < q0.w || yy > q1.x)) {
-                        t_best = t;
-                        hit = i;
-                        tag = __float_as_uint(q1.w);
-                    }
-                }
-            }
-        }
-    }
-    return HitOut{hit, tag, t_best};
-}
-
 // Closest hit over all n primitives of the flat table (PerformHit, Hittable.cuh:470-485, for each in turn), then
 // whether the reference's box culling could have answered differently.  Without culling the query returns the
 // geometric closest hit p* at t*; the reference returns it too unless (a) a box on p*'s path rejects the ray — its
@@ -2472,7 +2746,8 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
     }
     const bool tie = (tie_m >> __lane_id()) & 1u;
     if (tie || nan || edge || t_best != t_best) {
-        const HitOut r = ref_trace(rnodes, prims, ro, rd);
+        if (COUNT_TESTS) cnt.replays++;
+        const HitOut r = ref_trace<kRefStack>(rnodes, prims, ro, rd);
         hit = r.hit;
         tag = r.tag;
         t_best = r.t;
@@ -3183,6 +3458,15 @@ int acquire_queue(int device, uint32_t stride, uint32_t** head, int* cus) {
 
 using namespace rt;
 
+namespace {
+// Process-wide flags LaunchKernel adds to its own (rt_set_launch_flags); the environment's RT_LAUNCH_RANDOM_FILL=ltr sets
+// RT_FLAG_RIUS_LEFT_TO_RIGHT before the first call, so a viewer switches Random()'s fill order without a code change.
+std::atomic<uint32_t> g_launch_flags{0u};
+std::once_flag g_launch_env_once;
+constexpr uint32_t kLaunchFlagsAllowed = RT_FLAG_RIUS_LEFT_TO_RIGHT;
+
+}  // namespace
+
 extern "C" {
 
 int rt_set_wave_trace(void* buffer, uint64_t words) {
@@ -3552,10 +3836,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     std::shared_ptr<AutoChoice> trial;  // this frame is timed for the automatic choice: events ev[trial_slot..+1]
     int trial_slot = 0;
     const bool automatic = variant < 0 || variant >= kNumVariants;
-    // small scenes: the flat kernel takes v3's place (in the trial below 64 spp as well)
-    // (and up to kFlatMaxPrims primitives when rectangles touch other primitives: the flat kernels are exact there,
-    // the BVH kernels return the geometric closest hit, tests/adversarial_scene.py)
-    const bool flat_ok = S.prims_flat && (S.num_prims <= (uint32_t)g_flat_max || (S.touching_rects && g_flat_max > 0));
+    // small scenes: the flat kernel takes v3's place (in the trial below 64 spp as well).  (Until round 5 also scenes of
+    // up to kFlatMaxPrims primitives whose rectangles touch others, where only the flat kernels were exact; the BVH
+    // kernels now replay the reference traversal where it could differ, bvh_clear, and are faster beyond 16.)
+    const bool flat_ok = S.prims_flat && S.num_prims <= (uint32_t)g_flat_max;
     const int tile_kernel = flat_ok ? kVarFlat : kVarV3Compact;
     const int persistent_kernel = flat_ok ? kVarFlatPersistent : kVarV4;
     if (automatic) {
@@ -3647,6 +3931,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         return RT_ERR_UNSUPPORTED;
     }
     KernelFn fn = pick(variant, count_tests, S.has_textures, philox, wide, g_wave_trace != nullptr);
+    P.bvh_ref_nodes = (const float4*)S.bvh_ref_nodes;  // (the BVH kernels' exactness, bvh_clear)
+    P.bvh_boxes = (const float4*)S.bvh_boxes;
+    P.bvh_has_rects = S.has_rects ? 1u : 0u;
     if (V.kernel == 5 || V.kernel == 6) {  // the flat kernels' tables: primitives in the reference's test order, its BVH
         P.prims = (const float4*)S.prims_flat;
         P.ref_nodes = (const float4*)S.ref_nodes;
@@ -3789,9 +4076,22 @@ void LaunchRandInit(rt_curand_state* d_rand_state2) {
         hip_check(hipDeviceSynchronize(), "LaunchRandInit: hipDeviceSynchronize");
 }
 
+int rt_set_launch_flags(uint32_t flags) {
+    if (flags & ~kLaunchFlagsAllowed) {
+        set_error("rt_set_launch_flags: only RT_FLAG_RIUS_LEFT_TO_RIGHT may be set");
+        return RT_ERR_INVALID_ARGUMENT;
+    }
+    std::call_once(g_launch_env_once, [] {});  // (an explicit setting wins over the environment)
+    return (int)g_launch_flags.exchange(flags);
+}
+
 void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int image_height,
                   const unsigned int samples_per_pixel, const unsigned int max_depth, const void* world,
                   rt_curand_state* d_rand_state, rt_input_struct inputs) {
+    std::call_once(g_launch_env_once, [] {
+        const char* e = std::getenv("RT_LAUNCH_RANDOM_FILL");
+        if (e && std::strcmp(e, "ltr") == 0) g_launch_flags.store(RT_FLAG_RIUS_LEFT_TO_RIGHT);
+    });
     // The viewer mutates the graph in place between frames: the cache re-flattens it on
     // every call and updates the device scene by what changed (reference_scene_for_launch, api.cpp).
     std::shared_ptr<rt_scene> cached;  // held until the frame is done (another thread may evict the entry)
@@ -3807,7 +4107,7 @@ void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int imag
     a.height = image_height;
     a.samples_per_pixel = samples_per_pixel;
     a.max_depth = max_depth;
-    a.flags = RT_FLAG_FAITHFUL_GRID;
+    a.flags = RT_FLAG_FAITHFUL_GRID | g_launch_flags.load();
     a.tiling.band_rows = image_height ? image_height : 1;
     a.tiling.num_ranks = 1;
     a.tiling.rank = 0;

@@ -49,6 +49,9 @@ extern thread_local int g_texel_bytes;  // rt_set_tuning(RT_TUNE_TEXEL_LAYOUT): 
 constexpr int kRegStackDepth = 24;  // depth limit of the register (shift) traversal stack
 constexpr uint32_t kFlatMaxPrims = 64;  // scenes up to this many primitives also get the flat kernel's tables
 constexpr uint32_t kRefTreeMaxDepth = 14;  // deepest reference BVH the flat kernel replays (render.hip kRefStack)
+// ... and the BVH kernels (render.hip kRefStackBvh).  The reference tree splits at most 3 times by type and otherwise
+// in the middle, so 2^26 primitives (the library's limit) give depth <= 3 + 26 + 1.
+constexpr uint32_t kRefTreeMaxDepthBvh = 31;
 
 struct HostScene {
     std::vector<float> nodes;   // 16 floats per node
@@ -68,6 +71,8 @@ struct HostScene {
     uint32_t depth = 0;          // max root-to-leaf node count
     bool has_image_textures = false;
     bool has_textures = false;  // any CHECKER or IMAGE albedo
+    bool has_rects = false;     // any active rectangle (render.hip bvh_clear: only rectangles can turn a miss into a
+                                // NaN hit of the reference's)
     std::vector<int32_t> prim_source;  // desc index of each primitive (BVH order)
     std::vector<float> prims_flat;     // scenes of <= kFlatMaxPrims primitives: the records in the reference BVH's
                                        // test order (the flat kernel's table), else empty
@@ -76,9 +81,9 @@ struct HostScene {
                                        // check: 8 floats (scene_build.cpp)
     uint32_t flat_runs[2] = {0u, 0u};  // prims_flat holds each primitive type as one contiguous run: [begin, end) of
                                         // type t in bytes 2t, 2t + 1 of the pair (t = RT_SPHERE .. RT_YZRECT)
-    bool touching_rects = false;       // a rectangle's reference box touches or overlaps another primitive's: rays
-                                       // there can tie or graze a box face (the automatic choice keeps such scenes
-                                       // of <= kFlatMaxPrims primitives on the exact flat kernels)
+    std::vector<float> bvh_ref_nodes;  // every scene: the reference BVH (ref_nodes' layout) with its primitive children
+                                       // as ~(BVH-order index) — the BVH kernels' replay (render.hip bvh_clear)
+    std::vector<float> bvh_boxes;      // ... and per BVH-order primitive its reference box: (lo.xyz, 0), (hi.xyz, 0)
 };
 
 // Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.  with_texels = false computes

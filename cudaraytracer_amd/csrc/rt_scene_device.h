@@ -17,7 +17,8 @@ struct DeviceScene {
     const void* prims_flat = nullptr;  // the same records in the reference BVH's test order (small scenes), or NULL
     const void* ref_nodes = nullptr;   // the reference BVH (boxes + shape) over prims_flat, or NULL
     const void* flat_boxes = nullptr;  // per prims_flat record its reference box (exactness check), or NULL
-    bool touching_rects = false;       // HostScene::touching_rects
+    const void* bvh_ref_nodes = nullptr;  // the reference BVH over `prims` (BVH order), or NULL (bvh_clear, render.hip)
+    const void* bvh_boxes = nullptr;      // per `prims` record its reference box, or NULL
     uint32_t flat_runs[2] = {0u, 0u};  // HostScene::flat_runs
     const void* mats = nullptr;    // float4 × 3 per material
     const void* imgs = nullptr;    // int4 per image
@@ -26,6 +27,7 @@ struct DeviceScene {
     uint32_t num_imgs = 0;  // image descriptors (int4 each)
     bool has_image_textures = false;
     bool has_textures = false;  // any CHECKER or IMAGE albedo (selects the texture-capable kernel)
+    bool has_rects = false;     // HostScene::has_rects
     uint64_t device_bytes = 0;
 };
 

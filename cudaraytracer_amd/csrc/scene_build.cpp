@@ -267,11 +267,23 @@ void pack_flat_box(const rt_hittable_desc& h, float* o) {
     o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2]; o[3] = kl;
     o[4] = hi[0]; o[5] = hi[1]; o[6] = hi[2]; o[7] = kh;
 }
+// The BVH kernels' exactness check (render.hip bvh_clear) per BVH-order primitive: (lo.xyz, 0), (hi.xyz, 0) — its own
+// reference box as the reference's BoundingBox computes it (the innermost box on its path through the reference tree)
+void pack_ref_box(const rt_hittable_desc& h, float* o) {
+    float lo[3], hi[3];
+    ref_prim_box(h, lo, hi);
+    o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2]; o[3] = 0.0f;
+    o[4] = hi[0]; o[5] = hi[1]; o[6] = hi[2]; o[7] = 0.0f;
+}
 int build_reference_tree(const rt_hittable_desc* h, std::vector<int>& objs, int b, int e, uint32_t depth,
                          std::vector<RefNode>* nodes) {
     const int id = (int)nodes->size();
     nodes->push_back(RefNode());
-    std::stable_sort(objs.begin() + b, objs.begin() + e, [&](int x, int y) { return h[x].type < h[y].type; });
+    // (a range already in type order — every range below the root, whose sort left it so — is its own stable sort:
+    // skipped, so a scene of n primitives builds in O(n log n))
+    const auto by_type = [&](int x, int y) { return h[x].type < h[y].type; };
+    if (!std::is_sorted(objs.begin() + b, objs.begin() + e, by_type))
+        std::stable_sort(objs.begin() + b, objs.begin() + e, by_type);
     const int span = e - b;
     int c0, c1;
     if (span <= 2) {
@@ -467,6 +479,7 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
             *err = "hittable " + std::to_string(i) + ": negative sphere radius";
             return RT_ERR_INVALID_SCENE;
         }
+        out->has_rects = out->has_rects || !sphere;
         BuildPrim p;
         p.box = prim_box(h);
         for (int a = 0; a < 3; a++) p.centroid[a] = 0.5f * (p.box.lo[a] + p.box.hi[a]);
@@ -562,36 +575,44 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
         out->prim_source[i] = B.prims[B.order[i]].src;
         pack_prim(desc->hittables[out->prim_source[i]], out->prims.data() + (size_t)i * 8);
     }
+    if (out->num_prims == 0) return RT_OK;
+    // The reference's own BVH (its boxes and shape, Hittable.cuh:303-385) over the active primitives in list order.
+    std::vector<int> objs;
+    for (const BuildPrim& p : B.prims) objs.push_back(p.src);
+    std::vector<RefNode> rn;
+    build_reference_tree(desc->hittables, objs, 0, (int)objs.size(), 1, &rn);
+    uint32_t rdepth = 0;
+    for (const RefNode& n : rn) rdepth = std::max(rdepth, n.depth);
+    // Every scene: the reference BVH with its primitive children as ~(BVH-order index) and, per BVH-order primitive,
+    // its reference box — the BVH kernels' exactness check (render.hip bvh_clear): the rare rays whose closest hit the
+    // reference's box culling or an exact tie could change replay the reference BVH over the BVH-order records.
+    if (rdepth <= kRefTreeMaxDepthBvh) {
+        std::vector<int> bvh_index(desc->num_hittables, -1);
+        for (uint32_t i = 0; i < out->num_prims; i++) bvh_index[out->prim_source[i]] = (int)i;
+        out->bvh_boxes.resize((size_t)out->num_prims * 8);
+        for (uint32_t i = 0; i < out->num_prims; i++)
+            pack_ref_box(desc->hittables[out->prim_source[i]], out->bvh_boxes.data() + (size_t)i * 8);
+        out->bvh_ref_nodes.resize(rn.size() * 8);
+        for (size_t i = 0; i < rn.size(); i++) {
+            float* o = out->bvh_ref_nodes.data() + i * 8;
+            for (int k = 0; k < 2; k++) {
+                const int c = rn[i].child[k];
+                const int enc = c >= 0 ? c : ~bvh_index[~c];
+                for (int a = 0; a < 3; a++) o[4 * k + a] = k == 0 ? rn[i].lo[a] : rn[i].hi[a];
+                o[4 * k + 3] = bits_to_float((uint32_t)enc);
+            }
+        }
+    }
     // Small scenes: the primitives once more, in the order the reference's own BVH tests them (the flat kernel,
     // render.hip, tests every primitive of every ray in this order, so its closest hit breaks exact ties in t as
     // the reference's does)
     // together with the reference's own BVH (ref_nodes: its boxes and shape), which the flat kernel replays exactly
     // for the rare rays whose closest hit lies on a box face or ties (render.hip, ref_trace)
-    if (out->num_prims >= 1 && out->num_prims <= kFlatMaxPrims) {
-        std::vector<int> objs;
-        for (const BuildPrim& p : B.prims) objs.push_back(p.src);
-        std::vector<RefNode> rn;
-        build_reference_tree(desc->hittables, objs, 0, (int)objs.size(), 1, &rn);
-        uint32_t rdepth = 0;
-        for (const RefNode& n : rn) rdepth = std::max(rdepth, n.depth);
+    if (out->num_prims <= kFlatMaxPrims) {
         if (rdepth <= kRefTreeMaxDepth) {
             std::vector<int> ord;
             reference_test_order(rn, 0, &ord);
             std::vector<int> flat_index(desc->num_hittables, -1);
-            // a rectangle whose reference box touches or overlaps another primitive's (closed intervals on every
-            // axis): coplanar or abutting rectangles, walls meeting, a sphere resting on a floor
-            std::vector<std::array<float, 6>> boxes(ord.size());
-            for (size_t i = 0; i < ord.size(); i++) ref_prim_box(desc->hittables[ord[i]], boxes[i].data(), boxes[i].data() + 3);
-            for (size_t i = 0; i < ord.size() && !out->touching_rects; i++) {
-                if (desc->hittables[ord[i]].type == RT_SPHERE) continue;
-                for (size_t j = 0; j < ord.size() && !out->touching_rects; j++) {
-                    if (j == i) continue;
-                    bool touch = true;
-                    for (int a = 0; a < 3; a++)
-                        touch = touch && boxes[i][a] <= boxes[j][3 + a] && boxes[j][a] <= boxes[i][3 + a];
-                    out->touching_rects = touch;
-                }
-            }
             out->prims_flat.resize(ord.size() * 8);
             out->flat_boxes.resize(ord.size() * 8);
             for (size_t i = 0; i < ord.size(); i++) {

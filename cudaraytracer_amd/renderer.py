@@ -124,8 +124,10 @@ class Renderer:
         if radiance and self.radiance is None:
             self.radiance = torch.zeros(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
         if flags & abi.RT_FLAG_ACCUMULATE:
-            if self.accum is None:  # (never read before the first frame writes it)
-                self.accum = torch.empty(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
+            if self.accum is None:
+                # zeroed once: the first frame (RT_FLAG_ACCUMULATE_RESET) writes every pixel it renders, but with
+                # RT_FLAG_FAITHFUL_GRID the pixels outside whole 16×16 blocks are never rendered and must read 0
+                self.accum = torch.zeros(self.width * self.local_rows * 4, dtype=torch.float32, device=self.device)
                 self._accum_restart = True
             if self._accum_restart:
                 flags |= abi.RT_FLAG_ACCUMULATE_RESET

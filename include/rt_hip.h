@@ -153,6 +153,13 @@ void LaunchKernel(unsigned int* pos, unsigned int image_width, unsigned int imag
                   const unsigned int samples_per_pixel, const unsigned int max_depth, const void* world,
                   rt_curand_state* d_rand_state, rt_input_struct inputs);
 
+/* Flags LaunchKernel adds to its own (RT_FLAG_FAITHFUL_GRID), process-wide: RT_FLAG_RIUS_LEFT_TO_RIGHT selects the
+ * left-to-right fill of Random()'s Vec3(ξ, ξ, ξ) (Utils/Math.cuh:231-234; default right to left)
+ * for a viewer whose CUDA build filled it that way.  Any other bit is rejected (RT_ERR_INVALID_ARGUMENT).  Returns the
+ * previous flags.  Without a call, the environment variable RT_LAUNCH_RANDOM_FILL=ltr sets the same flag when
+ * LaunchKernel first runs. */
+int rt_set_launch_flags(uint32_t flags);
+
 /* Replaces `extern "C" void LaunchRandInit(curandState* d_rand_state2)` — Kernel.cu:193-197
  * (curand_init(1984, 0, 0) of one state). */
 void LaunchRandInit(rt_curand_state* d_rand_state2);
@@ -172,6 +179,11 @@ const char* rt_last_error(void);
 
 /* Library version string. */
 const char* rt_version(void);
+
+/* Version of this C ABI (structure layouts, counter words, entry points); a caller built against an older header
+ * can refuse a newer library.  6: RT_COUNTERS_WORDS (24) counter words with RT_FLAG_COUNT_TESTS, rt_set_launch_flags. */
+#define RT_ABI_VERSION 6
+int rt_abi_version(void);
 
 /* hipSetDevice on the calling thread. */
 int rt_set_device(int device);
@@ -267,15 +279,19 @@ typedef struct rt_render_args {
     float* radiance;          /* optional device float[local_rows·width·4]: pre-gamma mean colour (col/spp) */
     float* accum;             /* RT_FLAG_ACCUMULATE: device float4 running sum of samples */
     rt_curand_state* state;   /* device RNG states, local_rows × width (RT_FLAG_STATE_SOA: the six planes) */
-    uint64_t* counters;       /* optional device uint64[16]: rays, box tests, primitive tests, primary samples;
-                                 with RT_FLAG_COUNT_TESTS it must hold RT_COUNTERS_WORDS (24) words:
+    uint64_t* counters;       /* optional device uint64[RT_COUNTERS_WORDS] with RT_FLAG_COUNT_TESTS (the
+                                 kernels then write up to word 17; ABI versions < 6 wrote 16 words: see
+                                 rt_abi_version), else uint64[16]: rays, box tests, primitive tests, primary samples;
+                                 with RT_FLAG_COUNT_TESTS
                                  also [4..6] = wave-level iterations of node visits,
                                  primitive tests and shading (SIMD-efficiency diagnostics) and, for the v3
                                  kernels, [7..10] = wave clock cycles spent tracing, shading, in total and
                                  in leaves, [11..12] = node / primitive wave-iterations whose active lanes
                                  all test the same node / primitive, [13..15] = idle lanes per node iteration
                                  (pixel done, ray finished, holding a leaf), [16] = rectangle tests (the
-                                 part of [2] that are XY/XZ/YZRect::Hit; the FLOP model prices them apart) */
+                                 part of [2] that are XY/XZ/YZRect::Hit; the FLOP model prices them apart),
+                                 [17] = rays whose closest hit the exactness check replayed through the
+                                 reference BVH (render.hip bvh_clear / flat_trace) */
     uint32_t width;
     uint32_t height;          /* global image height */
     uint32_t samples_per_pixel;
@@ -372,10 +388,10 @@ int rt_last_variant(void);
  *   RT_TUNE_FLAT_MAX: scenes of at most this many active primitives (0..64, default 16) run the flat kernels
  *   (variants 5 and 6: no BVH, every ray tests every primitive in the reference BVH's test order, and rays whose
  *   answer the reference's box culling could change replay the reference BVH: the reference's pixels for any
- *   geometry) where the automatic choice would run variant 3 or 4; so do scenes of up to 64 primitives in which a
- *   rectangle's reference box touches another primitive's (coplanar, abutting or meeting rectangles, a sphere on a
- *   floor), unless the value is 0.  The BVH kernels return the geometric closest hit, which differs from the
- *   reference's only on exact ties and hits within rounding of a reference box face.  RT_TUNE_RIUS_TRIPS: the tile
+ *   geometry) where the automatic choice would run variant 3 or 4.  The BVH kernels (0-4) return the reference's
+ *   answer too: their closest hit is the geometric one, which can differ from the reference traversal's only on
+ *   exact ties, rays its own box test of the hit primitive rejects and rays with a zero or non-finite component, and
+ *   those rays replay the reference BVH (render.hip bvh_clear).  RT_TUNE_RIUS_TRIPS: the tile
  *   flat kernel (variant 5) makes at most this many RandomInUnitSphere attempts (Math.cuh:252-260) per shading pass; a
  *   lane whose attempts were all rejected continues the same call at the wave's next pass (0 = unbounded; 0..64;
  *   default 4; Philox mode rounds it up to whole blocks of four attempts).  RT_TUNE_RIUS_TRIPS_PERSISTENT: the same for

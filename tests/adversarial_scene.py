@@ -56,3 +56,22 @@ def adversarial_scene_large(extra: int = 12) -> scenes.Scene:
         h[i].type, h[i].is_active, h[i].material, h[i].radius = abi.RT_SPHERE, 1, k % 5, 0.15
         h[i].center[:] = [-1.8 + 0.35 * k, 1.6 + 0.1 * (k % 3), 0.8 + 0.2 * (k % 4)]
     return scenes.Scene(h, base.materials, [])
+
+
+def adversarial_scene_tiled(n: int = 8) -> scenes.Scene:
+    """The adversarial scene with its floor replaced by an n × n grid of abutting 1 × 1 floor tiles (XZRect, y = -1,
+    shared edges on every side) and a second, overlapping copy of its middle row (exact ties in t over the overlap):
+    8 + n·n + n primitives — beyond the flat kernels' 64 (kFlatMaxPrims), so only the BVH kernels render it, and its
+    touching geometry is where the reference's culling parts from the geometric closest hit."""
+    base = adversarial_scene()
+    tiles = [(x, z) for z in range(n) for x in range(n)] + [(x, n // 2) for x in range(n)]
+    nb = len(base.hittables)
+    h = (abi.HittableDesc * (nb + len(tiles)))()
+    for i in range(nb):
+        h[i] = base.hittables[i]
+    for k, (x, z) in enumerate(tiles):
+        i = nb + k
+        h[i].type, h[i].is_active, h[i].material = abi.RT_XZRECT, 1, (x + z + (k >= n * n)) % 5
+        h[i].center[:] = [-n / 2 + 0.5 + x, -1.0, -n / 2 + 2.5 + z]
+        h[i].width, h[i].height = 1.0, 1.0
+    return scenes.Scene(h, base.materials, [])

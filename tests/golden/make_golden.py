@@ -44,6 +44,29 @@ def digest(a: np.ndarray) -> bytes:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest()
 
 
+def row_digests(a: np.ndarray) -> np.ndarray:
+    """SHA-256 of each row of a (H, ...) array: (H, 32) uint8."""
+    return np.stack([np.frombuffer(digest(r), np.uint8) for r in a])
+
+
+def c4_frame_digests(threads: int = 8) -> None:
+    """BASELINE config 4's whole frame (7680×4320, 128 spp, depth 8, RTIOW, XORWOW, Random() right to left, one
+    rank) from the oracle's reference traversal: per row the SHA-256 of its RGBA8 pixels and of its pixels' advanced
+    RNG words (d, v[0..4]), and the frame's ray count — 276 KB instead of 133 MB of image and 800 MB of state
+    (tests/test_gpu_configs.py::test_c4_whole_frame_row_digests; ~3 min on 8 threads)."""
+    cfg = scenes.CONFIGS["c4"]
+    sc = scenes.builtin(cfg.scene)
+    st = po.init_states(cfg.width, cfg.height)
+    pos, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                            threads=threads)
+    words = st[:, :6].reshape(cfg.height, cfg.width, 6)
+    np.savez_compressed(os.path.join(HERE, "c4_frame_row_digests.npz"),
+                        config=np.array([cfg.width, cfg.height, cfg.spp, cfg.depth], np.uint32),
+                        pos_row_sha256=row_digests(pos), state_row_sha256=row_digests(words),
+                        counters=np.array([cnt.rays, cnt.box_tests, cnt.prim_tests, cnt.primary], np.uint64))
+    print("c4", pos.shape, cnt.rays, flush=True)
+
+
 def main(philox_only: bool = False) -> None:
     if philox_only:  # python tests/golden/make_golden.py --philox-only
         return philox_goldens()
@@ -94,4 +117,7 @@ def philox_goldens() -> None:
 
 
 if __name__ == "__main__":
-    main(philox_only="--philox-only" in sys.argv)
+    if "--c4" in sys.argv:  # python tests/golden/make_golden.py --c4   (the whole-frame C4 digests only)
+        c4_frame_digests()
+    else:
+        main(philox_only="--philox-only" in sys.argv)

@@ -32,6 +32,28 @@ def test_library_loads():
     assert lib().rt_version().startswith(b"librt_hip")
 
 
+def test_abi_version_matches_the_header():
+    """RT_COUNTERS_WORDS grew with RT_FLAG_COUNT_TESTS; the ABI version names such changes, and the library
+    reports the version of the header it was built from."""
+    hdr = open(os.path.join(ROOT, "include", "rt_hip.h")).read()
+    m = re.search(r"#define RT_ABI_VERSION (\d+)", hdr)
+    assert m and lib().rt_abi_version() == int(m.group(1)) >= 6
+    assert re.search(r"#define RT_COUNTERS_WORDS (\d+)u", hdr).group(1) == str(abi.COUNTERS_WORDS)
+
+
+def test_launch_flags_accept_only_the_fill_order():
+    """rt_set_launch_flags (LaunchKernel's Random() fill order): RT_FLAG_RIUS_LEFT_TO_RIGHT is
+    accepted and returned as the previous value; any other bit is refused without changing the setting."""
+    L = lib()
+    prev = L.rt_set_launch_flags(abi.RT_FLAG_RIUS_LEFT_TO_RIGHT)
+    try:
+        assert prev in (0, abi.RT_FLAG_RIUS_LEFT_TO_RIGHT)
+        assert L.rt_set_launch_flags(abi.RT_FLAG_RIUS_LEFT_TO_RIGHT | abi.RT_FLAG_RNG_PHILOX) < 0
+        assert L.rt_set_launch_flags(0) == abi.RT_FLAG_RIUS_LEFT_TO_RIGHT
+    finally:
+        L.rt_set_launch_flags(prev)
+
+
 def test_every_declared_symbol_is_exported():
     decl = declared_functions()
     assert decl == set(EXPORTED), (decl ^ set(EXPORTED))

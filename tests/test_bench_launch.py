@@ -21,7 +21,7 @@ def _bench(*args, timeout=240):
                           timeout=timeout, env=env, cwd=ROOT)
 
 
-@pytest.mark.parametrize("gpus, config", [(2, "c2"), (3, "c4")])
+@pytest.mark.parametrize("gpus, config", [(2, "c2"), (3, "c4"), (8, "c4")])
 def test_self_launch_spawns_n_ranks(gpus, config):
     p = _bench("--gpus", str(gpus), "--config", config, "--dry-run")
     assert p.returncode == 0, p.stderr[-2000:]
@@ -30,7 +30,7 @@ def test_self_launch_spawns_n_ranks(gpus, config):
     assert lines[0]["world_size"] == gpus and lines[0]["frame_ok"] is True
 
 
-@pytest.mark.parametrize("gpus", [2, 3])
+@pytest.mark.parametrize("gpus", [2, 3, 8])
 def test_default_line_carries_config4_block(gpus):
     """the driver's default `bench.py --gpus N` (config 2) also measures BASELINE config 4 (the
     7680x4320 frame split over the N ranks + the gather): the rehearsed launch carries other_configs.c4."""
@@ -39,6 +39,7 @@ def test_default_line_carries_config4_block(gpus):
     line = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")][0]
     c4 = line["other_configs"]["c4"]
     assert c4["frame_ok"] is True and c4["height"] == 4320 and c4["scaling"] == "strong"
+    assert line["world_size"] == gpus and line["frame_ok"] is True
 
 
 def test_fewer_gpus_than_requested_fails_loudly():

@@ -43,7 +43,7 @@ def _worker(rank: int, world: int, port: int, band_rows: int, out_path: str) -> 
     dist.destroy_process_group()
 
 
-def _pipelined_worker(rank: int, world: int, port: int, band_rows: int, out_path: str) -> None:
+def _pipelined_worker(rank: int, world: int, port: int, band_rows: int, out_path: str, height: int = 37) -> None:
     """BandGather as bench.py drives it: frame k's gather is started, frame k + 1 is "rendered" (the local
     buffer overwritten) before frame k is finished; rank 0 keeps every finished frame."""
     sys.path.insert(0, ROOT)
@@ -52,7 +52,7 @@ def _pipelined_worker(rank: int, world: int, port: int, band_rows: int, out_path
     from cudaraytracer_amd.renderer import band_rows_of
 
     parallel.init_process_group("gloo")
-    width, height = 5, 37
+    width = 5
     rows = torch.tensor(band_rows_of(height, band_rows, world, rank), dtype=torch.int64)
     local = torch.empty(len(rows) * width, dtype=torch.int64)
     g = parallel.BandGather(width, height, band_rows)
@@ -72,14 +72,16 @@ def _pipelined_worker(rank: int, world: int, port: int, band_rows: int, out_path
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world, band_rows", [(2, 16), (3, 4)])
-def test_pipelined_band_gather_keeps_frames_apart(tmp_path, world, band_rows):
+@pytest.mark.parametrize("world, band_rows, height", [(2, 16, 37), (3, 4, 37), (8, 16, 4320)])
+def test_pipelined_band_gather_keeps_frames_apart(tmp_path, world, band_rows, height):
+    """World size 8 with BASELINE config 4's 4320 rows in 16-row bands: 270 bands, so the last
+    round is ragged (ranks 0-5 hold 34 bands, 6 and 7 hold 33) — the 8-GPU scaling run's C4 gather."""
     out = str(tmp_path / "frames.npy")
-    mp.start_processes(_pipelined_worker, args=(world, _free_port(), band_rows, out), nprocs=world,
+    mp.start_processes(_pipelined_worker, args=(world, _free_port(), band_rows, out, height), nprocs=world,
                        start_method="spawn")
     frames = np.load(out)
-    base = np.arange(37 * 5).reshape(37, 5)
-    assert frames.shape == (4, 37, 5)
+    base = np.arange(height * 5).reshape(height, 5)
+    assert frames.shape == (4, height, 5)
     for k in range(4):
         np.testing.assert_array_equal(frames[k], base + 1000 * k)
 

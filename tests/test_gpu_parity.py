@@ -180,6 +180,89 @@ def test_drop_in_launchers_match_oracle():
     np.testing.assert_array_equal(pos.cpu().numpy().view(np.uint32).reshape(H, W), ref2)
 
 
+def _launch_kernel(sc, cfg, spp=None):
+    """LaunchRenderInit + LaunchKernel(world graph) of `sc` (Kernel.cu:178-204); returns (image, states)."""
+    dev = torch.device("cuda", 0)
+    W, H = cfg.width, cfg.height
+    pos = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    state = torch.zeros(W * H * abi.STATE_WORDS, dtype=torch.int32, device=dev)
+    lib().LaunchRenderInit(abi.Dim3(W // 16, H // 16, 1), abi.Dim3(16, 16, 1), W, H, C.c_void_p(state.data_ptr()))
+    graph = refgraph.build_graph(sc)
+    lib().LaunchKernel(C.c_void_p(pos.data_ptr()), W, H, spp or cfg.spp, cfg.depth,
+                       C.c_void_p(C.addressof(graph.world)), C.c_void_p(state.data_ptr()), cfg.inputs())
+    return (pos.cpu().numpy().view(np.uint32).reshape(H, W),
+            state.cpu().numpy().view(np.uint32).reshape(-1, abi.STATE_WORDS))
+
+
+@pytest.mark.parametrize("order", ["rtl", "ltr"])
+def test_launch_kernel_fill_order_switch(order):
+    """the drop-in LaunchKernel honours rt_set_launch_flags(RT_FLAG_RIUS_LEFT_TO_RIGHT) — a viewer
+    whose CUDA build filled Random()'s Vec3 left to right (Math.cuh:231-234) switches without leaving LaunchKernel —
+    and each order matches the oracle's same rius_order, bit for bit (image and RNG states)."""
+    case = CASE_BY_NAME["default_world_160x120_s8"]
+    cfg = case.cfg()
+    sc = scenes.builtin(cfg.scene)
+    flag, rius = (0, 1) if order == "rtl" else (abi.RT_FLAG_RIUS_LEFT_TO_RIGHT, 0)
+    prev = lib().rt_set_launch_flags(flag)
+    try:
+        img, states = _launch_kernel(sc, cfg)
+    finally:
+        lib().rt_set_launch_flags(prev)
+    st = po.init_states(cfg.width, cfg.height, full=False)
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                          faithful_grid=True, rius_order=rius)
+    np.testing.assert_array_equal(img, ref)
+    np.testing.assert_array_equal(states[:, :6], st[:, :6])
+    other, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(),
+                            po.init_states(cfg.width, cfg.height, full=False), faithful_grid=True, rius_order=1 - rius)
+    assert (other != ref).sum() > 100  # the two orders are different streams
+
+
+def test_launch_kernel_large_touching_scene_is_the_reference():
+    """a scene beyond the flat kernels' 64 primitives whose rectangles abut and overlap (the viewer's
+    AddHittable grows scenes without limit, CudaLayer.cpp:918-1370) renders through the drop-in LaunchKernel — on the
+    BVH kernels — bit for bit as the oracle's reference traversal (box culling and ties included), not as the
+    geometric closest hit, which differs on it (tests/test_scene_adversarial.py)."""
+    from adversarial_scene import ADVERSARIAL_CONFIG, adversarial_scene_tiled
+    cfg, sc = ADVERSARIAL_CONFIG, adversarial_scene_tiled()
+    assert len(sc.hittables) > 64
+    img, states = _launch_kernel(sc, cfg)
+    assert lib().rt_last_variant() in (2, 3, 4)
+    st = po.init_states(cfg.width, cfg.height, full=False)
+    ref, _, _ = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                          faithful_grid=True)
+    bad = np.argwhere(img != ref)
+    assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
+    np.testing.assert_array_equal(states[:, :6], st[:, :6])
+
+
+@pytest.mark.parametrize("rng", ["xorwow", "philox"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_bvh_kernels_exact_on_the_tiled_touching_scene(variant, rng):
+    """The BVH kernels' exactness check and replay (render.hip bvh_clear) on every BVH variant, both RNG modes, on the
+    > 64-primitive touching scene: whole frame, RNG states and ray count equal the oracle's reference traversal; the
+    counting build reports how many rays replayed (counters[17]) — a small fraction even here."""
+    from adversarial_scene import ADVERSARIAL_CONFIG, adversarial_scene_tiled
+    cfg, sc = ADVERSARIAL_CONFIG, adversarial_scene_tiled()
+    lib().rt_set_variant(variant)
+    r = Renderer(cfg.width, cfg.height, rng=rng)
+    r.render_init()
+    r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), frame=2, flags=abi.RT_FLAG_COUNT_TESTS)
+    torch.cuda.synchronize()
+    philox = rng == "philox"
+    assert lib().rt_last_variant() == (3 if philox and variant in (0, 1) else variant)
+    st = None if philox else po.init_states(cfg.width, cfg.height)
+    ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
+                            philox=philox, seed=1984, frame=2)
+    bad = np.argwhere(r.image() != ref)
+    assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
+    if not philox:
+        np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
+    rays, replays = int(r.counters[0]), int(r.counters[17])
+    assert rays == cnt.rays
+    assert 0 < replays < rays // 4, (replays, rays)  # (its duplicated row ties on every ray that hits it)
+
+
 def test_material_update_without_rebuild():
     case = CASE_BY_NAME["c2_rtiow_ragged_100x37_s4"]
     cfg = case.cfg()
@@ -623,16 +706,17 @@ def _small_rects_scene():
 
 
 @pytest.mark.parametrize("rng", ["xorwow", "philox"])
-@pytest.mark.parametrize("variant", [5, 6])
-def test_flat_kernels_exact_on_ties_and_box_faces(variant, rng):
-    """The flat kernels' exactness argument (render.hip flat_trace: a geometric closest hit is the reference's unless
+@pytest.mark.parametrize("variant", [5, 6, 0, 1, 2, 3, 4])
+def test_kernels_exact_on_ties_and_box_faces(variant, rng):
+    """The exactness argument (render.hip flat_trace and bvh_clear: a geometric closest hit is the reference's unless
     it ties, lies within rounding of a face of its own reference box, or a NaN took part — those rays replay the
     reference BVH) on a scene built to hit every case: coplanar rectangles that overlap (exact ties in t over an
     area) and abut (shared edges), a floor and a wall meeting their edges, spheres tangent to the rectangles'
     plane and touching the floor and wall with their box faces, a mirror sphere for reflected rays.  In this scene the
     reference's box culling changes 521 pixels against the brute-force closest hit (tests/test_scene_adversarial.py
     pins that on the CPU), so the whole frame, the RNG states and the ray count must equal the oracle's reference
-    traversal, not the geometric answer."""
+    traversal, not the geometric answer — on the flat kernels (5, 6) and, since round 6, on the BVH kernels (0-4)
+    whose SAH tree is not the reference's (v1/v2 have no Philox build: rt_render runs the compact v3 there)."""
     from adversarial_scene import ADVERSARIAL_CONFIG, adversarial_scene
     cfg, sc = ADVERSARIAL_CONFIG, adversarial_scene()
     lib().rt_set_variant(variant)
@@ -640,7 +724,7 @@ def test_flat_kernels_exact_on_ties_and_box_faces(variant, rng):
     r.render_init()
     r.render(DeviceScene(sc), cfg.spp, cfg.depth, cfg.inputs(), frame=3)
     torch.cuda.synchronize()
-    assert lib().rt_last_variant() == variant
+    assert lib().rt_last_variant() == (3 if rng == "philox" and variant in (0, 1) else variant)
     philox = rng == "philox"
     st = None if philox else po.init_states(cfg.width, cfg.height)
     ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st,
@@ -654,11 +738,12 @@ def test_flat_kernels_exact_on_ties_and_box_faces(variant, rng):
 
 
 @pytest.mark.parametrize("spp", [4, 64])
-def test_touching_rectangles_keep_larger_scenes_on_the_exact_kernels(spp):
-    """A scene beyond RT_TUNE_FLAT_MAX (20 primitives) whose rectangles touch (the adversarial scene plus 12 spheres):
-    the automatic choice keeps it on the flat kernels (both sides of the spp rule: the persistent one below 64 spp
-    after its trial, the tile one from 64), so the whole frame is the reference's; the 17-primitive startup world,
-    whose one rectangle touches nothing, stays on the BVH kernels."""
+def test_touching_rectangles_beyond_the_flat_limit_run_exact_bvh_kernels(spp):
+    """A scene beyond RT_TUNE_FLAT_MAX (20 primitives) whose rectangles touch (the adversarial scene plus 12 spheres).
+    Until round 5 the automatic choice kept such scenes on the flat kernels, the only exact ones; since the BVH kernels
+    replay the reference traversal for the rays where it could differ (render.hip bvh_clear), it runs them (faster at
+    this size), on both sides of the spp rule — the persistent one below 64 spp after its trial, the tile one from 64 —
+    and the whole frame is still the reference's."""
     from adversarial_scene import ADVERSARIAL_CONFIG, adversarial_scene_large
     cfg = ADVERSARIAL_CONFIG.scaled(ADVERSARIAL_CONFIG.width, ADVERSARIAL_CONFIG.height, spp)
     sc = adversarial_scene_large()
@@ -672,16 +757,10 @@ def test_touching_rectangles_keep_larger_scenes_on_the_exact_kernels(spp):
     for _ in range(frames):
         r.render(ds, cfg.spp, cfg.depth, cfg.inputs())
         torch.cuda.synchronize()
-        assert lib().rt_last_variant() in (5, 6)
+        assert lib().rt_last_variant() in (2, 3, 4)
         ref, _, cnt = po.render(po.OracleScene(sc), cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.inputs(), st)
         np.testing.assert_array_equal(r.image(), ref)
     np.testing.assert_array_equal(r.states()[:, :6], st[:, :6])
-    dw = scenes.CONFIGS["default"]
-    r2 = Renderer(64, 48)
-    r2.render_init()
-    r2.render(DeviceScene(scenes.builtin(dw.scene)), 64, 4, dw.inputs())
-    torch.cuda.synchronize()
-    assert lib().rt_last_variant() in (2, 3)
 
 
 @pytest.mark.parametrize("variant", KEY_VARIANTS + [0, 1])

@@ -21,3 +21,20 @@ def test_reference_culling_changes_pixels_in_the_adversarial_scene():
     differ = int((imgs[0] != imgs[1]).sum())
     assert differ > 100, differ
     assert len(np.unique(imgs[0])) > 1000  # the frame is not mostly sky
+
+
+def test_reference_culling_changes_pixels_in_the_tiled_adversarial_scene():
+    """The > 64-primitive variant (abutting floor tiles, an overlapping row) is adversarial too, and beyond the flat
+    kernels' tables: the GPU test that renders it through LaunchKernel (tests/test_gpu_parity.py::
+    test_launch_kernel_large_touching_scene_is_the_reference) runs the BVH kernels' exactness check and replay."""
+    from adversarial_scene import adversarial_scene_tiled
+    cfg, sc = ADVERSARIAL_CONFIG, adversarial_scene_tiled()
+    assert len(sc.hittables) > 64
+    imgs = []
+    for exact in (False, True):
+        st = po.init_states(cfg.width, cfg.height)
+        img, _, _ = po.render(po.OracleScene(sc, exact=exact), cfg.width, cfg.height, cfg.spp, cfg.depth,
+                              cfg.inputs(), st)
+        imgs.append(img)
+    differ = int((imgs[0] != imgs[1]).sum())
+    assert differ > 50, differ
