@@ -33,6 +33,7 @@ RT_TUNE_QUEUE_PREFETCH = 13
 RT_TUNE_QUEUE_GUIDE = 14
 RT_TUNE_QUEUE_MIN_CHUNK = 15
 RT_TUNE_RIUS_TRIPS_PERSISTENT = 16
+RT_TUNE_PREFETCH_STOP = 17
 
 STATUS = {
     0: "RT_OK",

@@ -263,6 +263,7 @@ struct KParams {
     const float4* bvh_ref_nodes;     // BVH kernels: the reference BVH over `prims` (bvh_clear), NULL = no replay
     const float4* bvh_boxes;         // BVH kernels: per `prims` record its reference box (bvh_clear)
     uint32_t bvh_has_rects;          // BVH kernels: the scene holds a rectangle (bvh_clear's check of misses)
+    uint32_t prefetch_stop;          // persistent flat: next pixels are taken ahead while the head holds > 1/this (0: never)
 };
 
 constexpr int kStackMax = 64;
@@ -316,6 +317,9 @@ constexpr float kTmin = 0.001f;  // color(): world->Hit(cur_ray, 0.001f, FLT_MAX
 constexpr float kSlabSlack = 1.0f + 0x1p-20f;
 // A hit index with this bit set (bvh_clear): a primitive tied with the closest hit so far (indices are < 2^26)
 constexpr int kTieBit = 0x40000000;
+#ifndef RT_REPLAY_SAME_PASS
+#define RT_REPLAY_SAME_PASS 0  // (A/B builds: 1 = v3 replays and shades flagged lanes in the pass that flagged them)
+#endif
 #ifndef RT_BVH_EXACT
 #define RT_BVH_EXACT 1  // (A/B builds only: 0 = the BVH kernels without the reference replay, the round-5 kernels;
                         //  2 = the tie tracking and the check without the replay; 3 = the tie tracking alone)
@@ -554,7 +558,7 @@ __device__ __noinline__ HitOut ref_trace(const float4* __restrict__ rnodes, cons
 // the BVH-order records, at a point of its loop where few registers are live: bvh_replay) and shades the answer, marked
 // kVerifiedBit (a verified miss: kVerifiedMiss), without a second check.
 constexpr int kVerifiedBit = 0x20000000;  // in a hit index: the reference traversal's own answer (bvh_replay)
-constexpr int kVerifiedMiss = -2;
+constexpr int kVerifiedMiss = 0x3fffffff;  // (flags 001 with an index no scene has: primitive indices are < 2^26)
 __device__ __forceinline__ bool bvh_odd_ray(const f3 ro, const f3 rd) {
     // (c): a direction component outside [2^-40, 2^40] in magnitude (zero, NaN and inf included: NaN fails every
     // comparison and propagates through the sum) or a non-finite origin
@@ -571,11 +575,11 @@ __device__ __forceinline__ bool bvh_odd_ray(const f3 ro, const f3 rd) {
 template <class PP>
 __device__ __forceinline__ bool bvh_clear(PP P, int& hit, const uint32_t tag, const float t, const f3 ro, const f3 rd,
                                           const float4 p0, const float4 p1, const f3 td, const f3 p, const f3 q) {
-    const bool miss = hit < 0;
-    const bool tie = !miss && (hit & kTieBit) != 0;
-    const bool verified = miss ? hit == kVerifiedMiss : (hit & kVerifiedBit) != 0;
+    // flags in bits 29-31 of the hit index: 000 a hit, 010 a tie, 001 verified, 111 a miss (-1); kVerifiedMiss
+    const uint32_t flags = (uint32_t)hit >> 29;
+    const bool miss = hit < 0 || hit == kVerifiedMiss, tie = flags == 2u, verified = flags == 1u;
     hit = miss ? -1 : (hit & (kVerifiedBit - 1));
-    if (RT_BVH_EXACT == 0 || RT_BVH_EXACT == 3 || verified || P->bvh_ref_nodes == nullptr) return true;
+    if (RT_BVH_EXACT == 0 || RT_BVH_EXACT == 3 || verified) return true;  // (bvh_ref_nodes: every scene, rt_render)
     bool clear;
     if (miss) {
         clear = !(P->bvh_has_rects && bvh_odd_ray(ro, rd));
@@ -586,7 +590,9 @@ __device__ __forceinline__ bool bvh_clear(PP P, int& hit, const uint32_t tag, co
         if (type == RT_SPHERE) {  // own box: centre -/+ radius (Hittable.cuh:112-116)
             const float r = p0.w;
             const float R = __builtin_fmaf(S, -0x1p-19f, r * (1.0f - 0x1p-19f));
-            clear = clear && fabsf(q.x) < R && fabsf(q.y) < R && fabsf(q.z) < R;
+            float qm;  // max |q_a| in one v_max3 (abs source modifiers; a NaN fails the comparison below)
+            asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(qm) : "v"(q.x), "v"(q.y), "v"(q.z));
+            clear = clear && qm < R;
         } else {  // own box: the extents, and k -/+ 0.0001 in the plane axis (Hittable.cuh:171-181, 227-237, 283-293)
             const float m = __builtin_fmaf(S, 0x1p-20f, 0x1p-100f);
             const bool yz = type == RT_YZRECT, xy = type == RT_XYRECT, xz = type == RT_XZRECT;
@@ -598,7 +604,7 @@ __device__ __forceinline__ bool bvh_clear(PP P, int& hit, const uint32_t tag, co
             clear = clear && in_rcp_range(dk) && (pa - p0.y) > m && (p0.z - pa) > m && (pb - p0.w) > m &&
                     (p1.x - pb) > m && (neg ? s1 : s0) < t && (neg ? s0 : s1) > t;
         }
-        if (!clear && !tie && t > kTmin && !bvh_odd_ray(ro, rd)) {
+        if (__builtin_expect(!clear && !tie && t > kTmin && !bvh_odd_ray(ro, rd), 0)) {
             // stage 2 (rare): AABB::Hit(own box, 0.001, t*) with the reference's arithmetic
             const float4* boxes = P->bvh_boxes;
             clear = ref_box(boxes[2 * hit], boxes[2 * hit + 1], ro, mk(rcp_rn(rd.x), rcp_rn(rd.y), rcp_rn(rd.z)), t);
@@ -856,14 +862,20 @@ __device__ __forceinline__ int shade(PP P, const float4* __restrict__ prims, con
     // hit_tag: the primitive's type | material << 4 word, which the traversal already read with the winning
     // primitive — the material load need not wait for the primitive's (nor for the exactness check)
     uint32_t mtype = 0xffu;  // 0xff: miss
-    if (hit >= 0) mtype = __float_as_uint(mats[3 * (hit_tag >> 4)].x) & 15u;
     if constexpr (EXACT) {
-        const int h = hit >= 0 ? (hit & (kVerifiedBit - 1)) : 0;
-        p0 = prims[2 * h + 0];  // (the record of primitive 0 for a miss: read, never used)
+        // the hit record's and the material's loads first, both in flight during the check (a replayed hit is shaded
+        // by a later call); the record of primitive 0 for a miss: read, never used
+        const int h = (hit >= 0 && hit != kVerifiedMiss) ? (hit & (kVerifiedBit - 1)) : 0;
+        p0 = prims[2 * h + 0];
         p1 = prims[2 * h + 1];
+        uint32_t mword = 0xffu;
+        if (hit >= 0 && hit != kVerifiedMiss) mword = __float_as_uint(mats[3 * (hit_tag >> 4)].x);
         const f3 td = scale(t, rd);  // (the hit point and p - c: shared with the hit record below)
         const f3 ph = add(ro, td);
-        if (!bvh_clear(P, hit, hit_tag, t, ro, rd, p0, p1, td, ph, sub(ph, xyz(p0)))) return SHADE_REPLAY;
+        if (__builtin_expect(!bvh_clear(P, hit, hit_tag, t, ro, rd, p0, p1, td, ph, sub(ph, xyz(p0))), 0)) return SHADE_REPLAY;
+        mtype = hit >= 0 ? (mword & 15u) : 0xffu;
+    } else {
+        if (hit >= 0) mtype = __float_as_uint(mats[3 * (hit_tag >> 4)].x) & 15u;
     }
     const bool specular = mtype == RT_METAL || mtype == RT_DIELECTRIC;
     if (hit < 0) {  // sky (Kernel.cu:41-44)
@@ -1631,7 +1643,9 @@ __device__ __forceinline__ void bvh_replay_wave(PP P, const float4* __restrict__
         const int L = (int)__builtin_ctzll(need);
         need &= need - 1u;
         const auto bl = [L](const float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L)); };
-        const HitOut r = ref_trace_wave(P->bvh_ref_nodes, prims, mk(bl(ro.x), bl(ro.y), bl(ro.z)), mk(bl(rd.x), bl(rd.y), bl(rd.z)));
+        const HitOut r = RT_BVH_EXACT == 4 ? HitOut{-1, 0u, 0.0f}
+                                           : ref_trace_wave(P->bvh_ref_nodes, prims, mk(bl(ro.x), bl(ro.y), bl(ro.z)),
+                                                            mk(bl(rd.x), bl(rd.y), bl(rd.z)));
         if (__lane_id() == (uint32_t)L) {
             c.hit = RT_BVH_EXACT == 4 ? (c.hit >= 0 ? (c.hit | kVerifiedBit) : kVerifiedMiss)  // (A/B: no replay)
                                       : (r.hit >= 0 ? (r.hit | kVerifiedBit) : kVerifiedMiss);
@@ -2133,8 +2147,9 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
     const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t w_start = __builtin_amdgcn_s_memtime();
     while (true) {
-        // shade() returned SHADE_REPLAY for these lanes: the path state is parked, few registers are live
-        if (__ballot(c.mode == MODE_REPLAY) != 0u) bvh_replay_wave(kparams_reload(), prims, c, ro, rd, cnt, COUNT_TESTS);
+        // (RT_REPLAY_SAME_PASS = 0: shade() returned SHADE_REPLAY for these lanes last pass; the path state is parked)
+        if (!RT_REPLAY_SAME_PASS && __builtin_expect(__ballot(c.mode == MODE_REPLAY) != 0u, 0))
+            bvh_replay_wave(kparams_reload(), prims, c, ro, rd, cnt, COUNT_TESTS);
         const uint64_t t_a = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t ntrav = COUNT_TESTS ? (uint32_t)__popcll(__ballot(c.mode == MODE_TRAV)) : 64u;
         if (c.mode == MODE_TRAV) {
@@ -2145,43 +2160,48 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v3(const KPa
         }
         const uint64_t t_b = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += t_b - t_a;
-        if (c.mode == MODE_SHADE) {
-            R rng;
-            f3 col, att;
-            uint32_t sample, depth, rays;
-            v3_unpark<COMPACT, false>(park, rng, col, att, sample, depth, rays);
-            f3 contrib;
-            if (COUNT_TESTS) cnt.wshade += wave_leader();
-            KParamsC* const q = kparams_reload();
-            const int res = shade<TEX, false, true>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng,
-                                                    rtl, contrib);
-            bool ended = res == SHADE_ENDED;
-            if (res != SHADE_REPLAY && !ended && ++depth >= q->max_depth) {  // exceeded recursion (Kernel.cu:79)
-                ended = true;
-                contrib = mk(0.0f, 0.0f, 0.0f);
+        for (;;) {  // the shading pass, and once more for lanes whose hit the reference traversal replayed
+            if (c.mode == MODE_SHADE) {
+                R rng;
+                f3 col, att;
+                uint32_t sample, depth, rays;
+                v3_unpark<COMPACT, false>(park, rng, col, att, sample, depth, rays);
+                f3 contrib;
+                if (COUNT_TESTS) cnt.wshade += wave_leader();
+                KParamsC* const q = kparams_reload();
+                const int res = shade<TEX, false, true>(q, prims, q->mats, q->imgs, c.hit, c.tag, c.t_best, ro, rd, att, rng,
+                                                        rtl, contrib);
+                bool ended = res == SHADE_ENDED;
+                if (res != SHADE_REPLAY && !ended && ++depth >= q->max_depth) {  // exceeded recursion (Kernel.cu:79)
+                    ended = true;
+                    contrib = mk(0.0f, 0.0f, 0.0f);
+                }
+                if (res == SHADE_REPLAY) {  // (nothing changed: re-parked as it was, replayed at the loop's top)
+                    c.mode = MODE_REPLAY;
+                } else if (kItemsBuild && items && ended) {  // this sample into its pixel's sums; the lane takes the next item below
+                    const uint32_t q0 = quant12(contrib.x), q1 = quant12(contrib.y), q2 = quant12(contrib.z);
+                    if (q0) atomicAdd(item_sum(sample, 0), (unsigned long long)q0);
+                    if (q1) atomicAdd(item_sum(sample, 1), (unsigned long long)q1);
+                    if (q2) atomicAdd(item_sum(sample, 2), (unsigned long long)q2);
+                    park[8 * 64] += rays;
+                    rays = 0u;
+                    c.mode = MODE_NEED;
+                } else if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
+                    col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
+                             __uint_as_float(park[(PK_COL + 2) * 64]));
+                    v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
+                    park[(PK_COL + 0) * 64] = __float_as_uint(col.x);
+                    park[(PK_COL + 1) * 64] = __float_as_uint(col.y);
+                    park[(PK_COL + 2) * 64] = __float_as_uint(col.z);
+                } else {
+                    v3_start_trace<WIDE>(P.num_nodes, c, rays);
+                    if (COUNT_TESTS && P.ray_dump) dump_ray(P, depth == P.ray_dump_depth, ro, rd);
+                }
+                v3_park<COMPACT, false>(park, rng, col, att, sample, depth, rays);
             }
-            if (res == SHADE_REPLAY) {  // (nothing changed: re-parked as it was, replayed at the loop's top)
-                c.mode = MODE_REPLAY;
-            } else if (kItemsBuild && items && ended) {  // this sample into its pixel's sums; the lane takes the next item below
-                const uint32_t q0 = quant12(contrib.x), q1 = quant12(contrib.y), q2 = quant12(contrib.z);
-                if (q0) atomicAdd(item_sum(sample, 0), (unsigned long long)q0);
-                if (q1) atomicAdd(item_sum(sample, 1), (unsigned long long)q1);
-                if (q2) atomicAdd(item_sum(sample, 2), (unsigned long long)q2);
-                park[8 * 64] += rays;
-                rays = 0u;
-                c.mode = MODE_NEED;
-            } else if (ended) {  // the colour sum stays parked until a path ends (3 fewer VGPRs live through shade())
-                col = mk(__uint_as_float(park[(PK_COL + 0) * 64]), __uint_as_float(park[(PK_COL + 1) * 64]),
-                         __uint_as_float(park[(PK_COL + 2) * 64]));
-                v3_next_sample<WIDE>(P, x, g, contrib, rng, col, att, sample, depth, ro, rd, c, rays);
-                park[(PK_COL + 0) * 64] = __float_as_uint(col.x);
-                park[(PK_COL + 1) * 64] = __float_as_uint(col.y);
-                park[(PK_COL + 2) * 64] = __float_as_uint(col.z);
-            } else {
-                v3_start_trace<WIDE>(P.num_nodes, c, rays);
-                if (COUNT_TESTS && P.ray_dump) dump_ray(P, depth == P.ray_dump_depth, ro, rd);
-            }
-            v3_park<COMPACT, false>(park, rng, col, att, sample, depth, rays);
+            // (RT_REPLAY_SAME_PASS: the lanes shade() returned SHADE_REPLAY for replay now, every lane active, and shade)
+            if (!RT_REPLAY_SAME_PASS || __ballot(c.mode == MODE_REPLAY) == 0u) break;
+            bvh_replay_wave(kparams_reload(), prims, c, ro, rd, cnt, COUNT_TESTS);
         }
         if constexpr (kItemsBuild) {
             // lanes whose path ended take the next items (ballot + mbcnt rank on the wave-uniform counter)
@@ -2507,7 +2527,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
 
     while (true) {
         // shade() returned SHADE_REPLAY for these lanes: the path state is parked, few registers are live
-        if (__ballot(c.mode == MODE_REPLAY) != 0u) bvh_replay_wave(kparams_reload(), prims, c, ro, rd, cnt, COUNT_TESTS);
+        if (__builtin_expect(__ballot(c.mode == MODE_REPLAY) != 0u, 0))
+            bvh_replay_wave(kparams_reload(), prims, c, ro, rd, cnt, COUNT_TESTS);
         if (c.mode == MODE_TRAV) v3_traverse<COUNT_TESTS, NODES, PK_WORDS4 * 256u, WIDE>(nrsrc, NODES == NODES_64 ? P.nodes : P.nodes48, P.refs, prims, stk, threshold, ro, rd, c, cnt);
         R rng;
         f3 col, att;
@@ -3038,7 +3059,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
             });
             if (need) mode = MODE_DONE;
             if constexpr (kNext) {  // the next pixel of every lane that just started one: its state loads go out now
-                bool want = started && npix == kNone && queue.head_left > P.work_per_counter / kPrefetchStop;
+                bool want = started && npix == kNone && P.prefetch_stop != 0u &&
+                            queue.head_left > P.work_per_counter / P.prefetch_stop;
                 if (__ballot(want) != 0)
                     queue.take(P, want, [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {
                         nx = qx;
@@ -3294,6 +3316,9 @@ thread_local int g_leaf_break = 3;
 thread_local int g_flat_max = 16;
 thread_local int g_rius_trips = 4;
 thread_local int g_rius_trips_persistent = 0;
+// RT_TUNE_PREFETCH_STOP: the persistent flat kernel's lanes take their next pixel ahead (kFlatPrefetch) only while their
+// wave's queue head holds more than 1/value of its range (0 = never); kPrefetchStop (8) by default
+thread_local int g_prefetch_stop = (int)dev::kPrefetchStop;
 
 // Per (device, stream, tile grid): the tile costs the v3 kernel records and the order planned from them.
 // Plans are held by shared_ptr: a caller keeps its plan alive across the launch even if another thread
@@ -3651,6 +3676,15 @@ int rt_set_tuning(int key, int value) {
         knob = value;
         return prev;
     }
+    if (key == RT_TUNE_PREFETCH_STOP) {
+        if (value < 0 || value > 1024) {
+            set_error("rt_set_tuning: prefetch stop must be in [0, 1024]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_prefetch_stop;
+        g_prefetch_stop = value;
+        return prev;
+    }
     if (key == RT_TUNE_FLAT_MAX) {
         if (value < 0 || value > (int)kFlatMaxPrims) {
             set_error("rt_set_tuning: flat kernel primitive limit must be in [0, 64]");
@@ -3934,6 +3968,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.bvh_ref_nodes = (const float4*)S.bvh_ref_nodes;  // (the BVH kernels' exactness, bvh_clear)
     P.bvh_boxes = (const float4*)S.bvh_boxes;
     P.bvh_has_rects = S.has_rects ? 1u : 0u;
+    P.prefetch_stop = (uint32_t)g_prefetch_stop;
     if (V.kernel == 5 || V.kernel == 6) {  // the flat kernels' tables: primitives in the reference's test order, its BVH
         P.prims = (const float4*)S.prims_flat;
         P.ref_nodes = (const float4*)S.ref_nodes;

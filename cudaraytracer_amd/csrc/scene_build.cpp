@@ -586,7 +586,11 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
     // Every scene: the reference BVH with its primitive children as ~(BVH-order index) and, per BVH-order primitive,
     // its reference box — the BVH kernels' exactness check (render.hip bvh_clear): the rare rays whose closest hit the
     // reference's box culling or an exact tie could change replay the reference BVH over the BVH-order records.
-    if (rdepth <= kRefTreeMaxDepthBvh) {
+    if (rdepth > kRefTreeMaxDepthBvh) {  // (2^26 primitives give <= 30: not reached within the primitive limit above)
+        *err = "reference BVH deeper than " + std::to_string(kRefTreeMaxDepthBvh) + " levels";
+        return RT_ERR_INVALID_SCENE;
+    }
+    {
         std::vector<int> bvh_index(desc->num_hittables, -1);
         for (uint32_t i = 0; i < out->num_prims; i++) bvh_index[out->prim_source[i]] = (int)i;
         out->bvh_boxes.resize((size_t)out->num_prims * 8);

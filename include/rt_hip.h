@@ -402,13 +402,15 @@ int rt_last_variant(void);
  *   profiles/r05g_ab_c5_queue_prefetch.txt).  RT_TUNE_QUEUE_GUIDE: guided chunk sizes for
  *   the persistent kernels — a wave takes (its head's remaining indices) / (waves per head × this factor), rounded
  *   down to a multiple of 16, at least RT_TUNE_QUEUE_MIN_CHUNK (16..64) and at most RT_TUNE_QUEUE_CHUNK (0 = off:
- *   RT_TUNE_QUEUE_CHUNK while plenty is left, then 64; 0..64).  None of these changes the image. */
+ *   RT_TUNE_QUEUE_CHUNK while plenty is left, then 64; 0..64).  RT_TUNE_PREFETCH_STOP: the persistent flat kernel's lanes
+ *   take their next pixel (and its RNG state) ahead while their wave's queue head holds more than 1/value of its
+ *   range (default 8; 0 = never ahead; 0..1024).  None of these changes the image. */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
                      RT_TUNE_REGEN_LIVE_FRAC = 9, RT_TUNE_LEAF_BREAK = 10, RT_TUNE_RIUS_TRIPS = 11,
                      RT_TUNE_FLAT_MAX = 12, RT_TUNE_QUEUE_PREFETCH = 13, RT_TUNE_QUEUE_GUIDE = 14,
-                     RT_TUNE_QUEUE_MIN_CHUNK = 15, RT_TUNE_RIUS_TRIPS_PERSISTENT = 16 };
+                     RT_TUNE_QUEUE_MIN_CHUNK = 15, RT_TUNE_RIUS_TRIPS_PERSISTENT = 16, RT_TUNE_PREFETCH_STOP = 17 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

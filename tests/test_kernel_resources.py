@@ -34,8 +34,10 @@ def _v4(t, p, wd=0, trace=0):
 HOT = [_v3(t, p, c) for t in (0, 1) for p in (0, 1) for c in (0, 1)] + [_v4(t, p) for t in (0, 1) for p in (0, 1)] + \
       [_v3(t, p, 1, 1) for t in (0, 1) for p in (0, 1)] + [_v4(t, p, 1) for t in (0, 1) for p in (0, 1)]
 # register-held builds: a few bytes of cold spills (measured faster than the compiler's register count)
-# (the Philox build reserves 36 B of stack for SGPR spill slots its code never touches: no scratch instruction)
-SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 48}
+# (the Philox build reserves 36 B of stack for SGPR spill slots its code never touches: no scratch instruction; since
+# round 6 the textured XORWOW v4 likewise).  No v3/v4 build calls a function any more (the reference replay of
+# bvh_clear runs inline, ref_trace_wave), so none reserves a callee's frame.
+SPILL_OK = {_v3(0, 0, 1): 32, _v3(0, 1, 1): 48, _v4(1, 0): 36, _v4(1, 0, 1): 36}
 
 
 def kernel_metadata(tmp_path):
