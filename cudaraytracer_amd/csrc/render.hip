@@ -2499,6 +2499,8 @@ __device__ __forceinline__ void trace_persistent_wave(const KParams& P, const Pi
     }
 }
 
+// v4 persistent kernel.  It must not exit early: every wave runs to queue_release, whose last caller re-zeroes the
+// frame's queue slot for the launch that reuses it (render_kernel_flat_persistent has the same rule).
 template <bool COUNT_TESTS, bool TEX, int NODES = NODES_64, bool PHILOX = false, bool WIDE = false, int WAVES_PER_SIMD = 1,
           bool TRACE = false>
 __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KParams P) {
@@ -2929,7 +2931,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
 // of the current pixel is loaded when it starts, not when it is written.  The next pixel is taken early only while
 // the wave's queue head holds more than 1/kPrefetchStop of its range: near the end a pixel parked in a busy lane's
 // prefetch slot waits out that lane's current pixel while other lanes idle (always-on prefetch lengthened the tail
-// 168 -> 211 us; profiles/r04e_ab_c5_prefetch.txt).
+// 168 -> 211 us; profiles/r04e_ab_c5_prefetch.txt).  Like v4 it must not exit early: every wave reaches
+// queue_release, which leaves the queue slot zeroed for its next user.
 constexpr int kFlatPrefetch = 1;
 constexpr uint32_t kPrefetchStop = 8;
 template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD, bool TRACE = false>
@@ -4028,6 +4031,11 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     (void)hipGetLastError();
     hipLaunchKernelGGL(fn, dim3(grid), dim3(V.block), lds_bytes, s, P);
     int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
+    // A persistent launch that did not run leaves its queue slot as it found it, but the slot is re-zeroed anyway, so
+    // that the launch reusing it kQueueSlots launches later never finds exhausted heads (the slot is
+    // otherwise clean only because the grid's last wave zeroes it in queue_release)
+    if (rc != RT_OK && persistent)
+        (void)hipMemsetAsync(P.work_counter, 0, (size_t)(dev::kQueueCounters + 2u) * P.queue_stride * 4u, s);
     if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);  // the render kernel alone (v4 has no plan step)
     if (rc == RT_OK && plan) {  // the next launch on this stream dispatches this frame's costliest tiles first
         hipLaunchKernelGGL(dev::plan_order_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)plan->cost, plan->order,

@@ -569,7 +569,9 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
             out->refs[i] = ((uint32_t)n.child[0] & 0xffffu) | ((uint32_t)n.child[1] << 16);
         }
     }
-    out->prims.resize((size_t)out->num_prims * 8);
+    // (at least one record: the BVH kernels' shade() loads record 0 for a miss before it knows the ray missed, so an
+    // empty scene carries one zero record that no traversal reaches)
+    out->prims.assign((size_t)std::max(out->num_prims, 1u) * 8, 0.0f);
     out->prim_source.resize(out->num_prims);
     for (uint32_t i = 0; i < out->num_prims; i++) {
         out->prim_source[i] = B.prims[B.order[i]].src;
