@@ -28,6 +28,7 @@
 #include <cstring>
 #include <atomic>
 #include <map>
+#include <numeric>
 #include <memory>
 #include <mutex>
 #include <tuple>
@@ -264,6 +265,11 @@ struct KParams {
     const float4* bvh_boxes;         // BVH kernels: per `prims` record its reference box (bvh_clear)
     uint32_t bvh_has_rects;          // BVH kernels: the scene holds a rectangle (bvh_clear's check of misses)
     uint32_t prefetch_stop;          // persistent flat: next pixels are taken ahead while the head holds > 1/this (0: never)
+    uint32_t group_tiles;            // persistent flat, GROUP: tiles [0, group_tiles) are the workgroups' static shares
+    uint32_t queue_base;             // persistent kernels: the queue's first work index (GROUP: group_tiles * 64; v4: 0)
+    uint32_t group_perm_a;           // GROUP: 0 = interleaved shares; else the shares' golden-ratio step (GroupShare)
+    uint32_t group_perm_b, group_perm_k;  // ... (group_perm_k · group_perm_a) mod group_tiles, and tiles per share
+    uint32_t queue_host_reset;       // persistent kernels: 1 = rt_render zeroed the queue slot (no queue_release)
 };
 
 constexpr int kStackMax = 64;
@@ -2403,7 +2409,7 @@ struct PixelQueue {
                     if (__lane_id() == leader) base = atomicAdd(P.work_counter + qc * P.queue_stride, want);
                     base = __builtin_amdgcn_readlane(base, leader);
                 }
-                const uint32_t idx = qc * P.work_per_counter + base;
+                const uint32_t idx = P.queue_base + qc * P.work_per_counter + base;
                 if (TRACE) {  // (diagnostic: the atomic's round trip, stamped after its result is in)
                     __builtin_amdgcn_s_waitcnt(0);
                     rt_atomic += __builtin_amdgcn_s_memrealtime() - ta;
@@ -2469,12 +2475,18 @@ struct PixelQueue {
 // and the finished-waves count kQueueCounters + 1 strides in), so the slot is clean for the launch that reuses it and
 // rt_render needs no memset per frame (5 us per C5 frame, profiles/r04p_kernel_stats_by_grid_c5.csv).  Every wave
 // reaches this point after its last queue atomic has returned.
-__device__ __forceinline__ void queue_release(const KParams& P) {
+__device__ __forceinline__ uint32_t grid_waves() { return gridDim.x * (blockDim.x >> 6); }
+__device__ __forceinline__ uint32_t grid_wave_id() {  // (wave-uniform: an SGPR, not a per-lane value)
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+}
+// arrivals: how many callers the launch has (its waves, or — GROUP — its workgroups, whose last wave calls it)
+__device__ __forceinline__ void queue_release(const KParams& P, const uint32_t arrivals) {
+    if (P.queue_host_reset) return;
     const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
     uint32_t fin = 0u;
     if (__lane_id() == leader) fin = atomicAdd(P.work_counter + (kQueueCounters + 1u) * P.queue_stride, 1u);
     fin = __builtin_amdgcn_readlane(fin, leader);
-    if (fin == gridDim.x - 1u && __lane_id() < kQueueCounters + 2u)
+    if (fin == arrivals - 1u && __lane_id() < kQueueCounters + 2u)
         __hip_atomic_store(P.work_counter + __lane_id() * P.queue_stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2484,13 +2496,14 @@ __device__ __forceinline__ void queue_release(const KParams& P) {
 // << 32, [7] realtime ticks spent waiting for the queue's atomics.  Times: s_memrealtime (100 MHz).
 constexpr uint32_t kWaveTraceWords = 8;
 template <bool TRACE>
-__device__ __forceinline__ void trace_persistent_wave(const KParams& P, const PixelQueue<TRACE>& queue, uint64_t rt_start) {
-    if (TRACE && P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (blockIdx.x + 1ull) <= P.wave_trace_words) {
-        unsigned long long* w = P.wave_trace + (size_t)kWaveTraceWords * blockIdx.x;
+__device__ __forceinline__ void trace_persistent_wave(const KParams& P, const PixelQueue<TRACE>& queue, uint64_t rt_start,
+                                                      uint32_t wave_pixels) {
+    if (TRACE && P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (grid_wave_id() + 1ull) <= P.wave_trace_words) {
+        unsigned long long* w = P.wave_trace + (size_t)kWaveTraceWords * grid_wave_id();
         w[0] = rt_start;
         w[1] = queue.rt_drained;
         w[2] = __builtin_amdgcn_s_memrealtime();
-        w[3] = queue.wave_pixels | ((unsigned long long)gridDim.x << 32);
+        w[3] = wave_pixels | ((unsigned long long)grid_waves() << 32);
         w[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
                ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
         w[5] = queue.rt_last;
@@ -2593,8 +2606,8 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_v4(const KPa
     cnt.rays = park[PK_RAYS * 64];
     // every sample starts with one camera ray (Kernel.cu:137-146): spp primary rays per pixel taken
     cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;
-    trace_persistent_wave(P, queue, rt_start);
-    queue_release(P);
+    trace_persistent_wave(P, queue, rt_start, queue.wave_pixels);
+    queue_release(P, grid_waves());
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
@@ -2921,6 +2934,66 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
     finish_pixel<COUNT_TESTS>(P, pix, st, rng, col, cnt);
 }
 
+// The persistent flat kernel's workgroup share (GROUP builds, round 6).  One 16-wave workgroup per CU owns a static
+// interleaved share of the frame's 8×8 tiles — tile k for k ≡ group (mod groups), k < P.group_tiles — and hands its
+// positions (64 per tile, in order) to whichever of its 1 024 lanes needs a pixel through one LDS counter: a
+// ds_add_rtn per take, no device-scope atomic, and no private reserve.  Today's per-wave queue keeps a reserve per wave
+// (its chunk of up to 128 indices, the chunk fetched ahead, and every lane's next pixel) that it hands out long after
+// the queue ran dry while other waves idle: C5's tail was 149 of 262 us (profiles/r05ad_c5_tail_final.txt).  The
+// tiles past group_tiles stay in the per-wave queue (PixelQueue over [queue_base, work_total)), which the waves turn
+// to once their group's share is handed out, so CUs that run slow or hold costly tiles are evened out at the end.
+struct GroupShare {
+    uint32_t* next;        // LDS: positions of the share handed out (may run past total)
+    uint32_t total;        // positions in the share
+    uint32_t left;         // positions left as of this wave's last take
+    bool done = false;     // wave-uniform: the share is handed out
+    __device__ GroupShare(const KParams& P, uint32_t* lds_next) : next(lds_next) {
+        const uint32_t lo = blockIdx.x * P.group_perm_k;  // (permuted: the share is j in [lo, lo + K) ∩ [0, S))
+        const uint32_t own = P.group_perm_a ? (lo < P.group_tiles ? min(P.group_perm_k, P.group_tiles - lo) : 0u)
+                           : blockIdx.x < P.group_tiles ? (P.group_tiles - 1u - blockIdx.x) / gridDim.x + 1u : 0u;
+        total = own * 64u;
+        left = total;
+        done = total == 0u;
+    }
+    // Lanes with `need` take the next positions (ballot + mbcnt rank); start(x, g, pix, idx) runs on every lane that
+    // gets a pixel.  A lane still needing one afterwards found the share handed out (done).
+    template <class F>
+    __device__ __forceinline__ uint32_t take(const KParams& P, bool& need, F&& start) {
+        uint64_t needm = __ballot(need);
+        uint32_t taken_px = 0u;
+        while (needm != 0 && !done) {
+            const uint32_t k = (uint32_t)__popcll(needm);
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)needm) - 1u;
+            uint32_t base = 0u;
+            if (__lane_id() == leader) base = __hip_atomic_fetch_add(next, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            base = __builtin_amdgcn_readlane(base, leader);
+            const uint32_t avail = base < total ? min(k, total - base) : 0u;
+            left = base < total ? total - base - avail : 0u;
+            if (avail < k) done = true;
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+            if (need && rank < avail) {
+                const uint32_t pos = base + rank;
+                // interleaved: tile g + k·groups; permuted: tile (j · A) mod S for j = g·K + k, i.e. (g·B + k·A) mod S
+                // (rt_render keeps both terms below 2^32 or leaves the shares interleaved)
+                const uint32_t tile = P.group_perm_a
+                                          ? (blockIdx.x * P.group_perm_b + (pos >> 6) * P.group_perm_a) % P.group_tiles
+                                          : blockIdx.x + (pos >> 6) * gridDim.x;
+                const uint32_t idx = tile * 64u + (pos & 63u);
+                uint32_t x, g, pix;
+                if (work_pixel(P, idx, x, g, pix)) {  // (a position outside the image: the lane takes another)
+                    need = false;
+                    start(x, g, pix, idx);
+                }
+            }
+            const uint64_t still = __ballot(need);
+            taken_px += (uint32_t)__popcll(needm & ~still);
+            needm = still;
+        }
+        return taken_px;
+    }
+};
+
 // Persistent flat kernel (variant 6): the flat kernel's closest-hit query in v4's persistent grid — a device-filling
 // grid whose lanes take the next pixel from the frame's work queue as soon as theirs is done (PixelQueue), for frames
 // with few samples per pixel (BASELINE config 5: 1 spp), where a tile wave would idle on its slowest pixels.  The path
@@ -2935,8 +3008,10 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
 // queue_release, which leaves the queue slot zeroed for its next user.
 constexpr int kFlatPrefetch = 1;
 constexpr uint32_t kPrefetchStop = 8;
-template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD, bool TRACE = false>
-__global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persistent(const KParams P) {
+// GROUP (round 6, the default): 1024-thread workgroups, one per CU, whose waves draw from the group's static share
+// first (GroupShare) and from the per-wave queue after it; !GROUP: one-wave workgroups on the per-wave queue alone.
+template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD, bool TRACE = false, bool GROUP = true>
+__global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kernel_flat_persistent(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     constexpr bool kNext = (kFlatPrefetch & 1) && !PHILOX;  // (Philox has no per-pixel state to load)
     constexpr bool kAcc = (kFlatPrefetch & 2) != 0;
@@ -2953,14 +3028,17 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     float4* const tboxes = tprims + 2u * P.num_prims;
     float4* const tmats = tboxes + 2u * P.num_prims;
     int4* const timgs = reinterpret_cast<int4*>(tmats + 3u * P.num_mats);
+    // GROUP: the share's LDS counter after the tables (rt_render sizes the LDS for it)
+    uint32_t* const share_next = reinterpret_cast<uint32_t*>(timgs + P.num_imgs);
     {
-        const uint32_t lane = threadIdx.x & 63u;
-        for (uint32_t i = lane; i < 2u * P.num_prims; i += 64u) {
+        const uint32_t tid = threadIdx.x, nt = blockDim.x;
+        for (uint32_t i = tid; i < 2u * P.num_prims; i += nt) {
             tprims[i] = prims[i];
             tboxes[i] = P.flat_boxes[i];
         }
-        for (uint32_t i = lane; i < 3u * P.num_mats; i += 64u) tmats[i] = P.mats[i];
-        for (uint32_t i = lane; i < P.num_imgs; i += 64u) timgs[i] = P.imgs[i];
+        for (uint32_t i = tid; i < 3u * P.num_mats; i += nt) tmats[i] = P.mats[i];
+        for (uint32_t i = tid; i < P.num_imgs; i += nt) timgs[i] = P.imgs[i];
+        if (GROUP && tid < 2u) share_next[tid] = 0u;  // (the share's counter, the group's finished waves)
         __syncthreads();
     }
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
@@ -2975,17 +3053,22 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
     int hit = -1;
     uint32_t tag = 0u;
     float t = FLT_MAX;
-    PixelQueue<TRACE> queue(blockIdx.x % kQueueCounters);
+    const uint32_t wave_id = grid_wave_id(), n_waves = grid_waves();
+    PixelQueue<TRACE> queue(wave_id % kQueueCounters);
+    GroupShare share(P, share_next);
+    if (!GROUP) share.done = true;
+    if (P.work_per_counter == 0u) queue.drained = true;  // (GROUP with no tail: every tile is in the shares)
+    uint32_t wave_pixels = 0u;  // pixels this wave took from its group's share
     const uint64_t rt_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0u;
     // pass trace (diagnostic, tools/c5_tail.py): every 64th wave stamps each of its first kPassTrace / 4 passes with 4
     // words: s_memrealtime at the pass start (bits 0-39) with the lanes about to trace (40-46), shade (47-53) and with a
     // pixel at all (54-60); then s_memrealtime after the trace, after the shading and after the queue
     constexpr uint32_t kPassTrace = 1024;
-    const bool pass_traced = TRACE && P.wave_trace && (blockIdx.x & 63u) == 0u &&
-                             (uint64_t)P.wave_trace_words >= (uint64_t)kWaveTraceWords * gridDim.x +
-                                 (uint64_t)kPassTrace * (blockIdx.x / 64u + 1u);
+    const bool pass_traced = TRACE && P.wave_trace && (wave_id & 63u) == 0u &&
+                             (uint64_t)P.wave_trace_words >= (uint64_t)kWaveTraceWords * n_waves +
+                                 (uint64_t)kPassTrace * (wave_id / 64u + 1u);
     unsigned long long* const pass_rec =
-        pass_traced ? P.wave_trace + (size_t)kWaveTraceWords * gridDim.x + (size_t)kPassTrace * (blockIdx.x / 64u) : nullptr;
+        pass_traced ? P.wave_trace + (size_t)kWaveTraceWords * n_waves + (size_t)kPassTrace * (wave_id / 64u) : nullptr;
     uint32_t pass_no = 0u;
     while (true) {
         life++;
@@ -3057,21 +3140,34 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
                     npix = kNone;
                 }
             }
-            queue.take(P, need, [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {  // Kernel.cu:119-123
+            const auto start_new = [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {  // Kernel.cu:119-123
                 start(qx, qg, qpix, qidx, begin_rng<R>(state_at(P, qpix), P.state_stride, qg * P.width + qx));
-            });
+            };
+            if (GROUP && !share.done) {
+                const uint32_t n = share.take(P, need, start_new);
+                wave_pixels += n;
+                if (TRACE && n) queue.rt_last = __builtin_amdgcn_s_memrealtime();  // (last pixel handed out)
+            }
+            if (__ballot(need) != 0) queue.take(P, need, start_new);
             if (need) mode = MODE_DONE;
             if constexpr (kNext) {  // the next pixel of every lane that just started one: its state loads go out now
-                bool want = started && npix == kNone && P.prefetch_stop != 0u &&
-                            queue.head_left > P.work_per_counter / P.prefetch_stop;
-                if (__ballot(want) != 0)
-                    queue.take(P, want, [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {
-                        nx = qx;
-                        ng = qg;
-                        npix = qpix;
-                        nwidx = qidx;
-                        nrng = load_rng(state_at(P, qpix), P.state_stride);
-                    });
+                const auto take_next = [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {
+                    nx = qx;
+                    ng = qg;
+                    npix = qpix;
+                    nwidx = qidx;
+                    nrng = load_rng(state_at(P, qpix), P.state_stride);
+                };
+                // (from the group's share while it holds more than 1/prefetch_stop of itself; then from the queue by
+                // the same rule on the wave's head)
+                bool want = started && npix == kNone && P.prefetch_stop != 0u;
+                if (GROUP && !share.done) {
+                    want = want && share.left > share.total / P.prefetch_stop;
+                    if (__ballot(want) != 0) wave_pixels += share.take(P, want, take_next);
+                } else {
+                    want = want && queue.head_left > P.work_per_counter / P.prefetch_stop;
+                    if (__ballot(want) != 0) queue.take(P, want, take_next);
+                }
             }
         }
         pass_stamp(3);
@@ -3086,9 +3182,20 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat_persist
         if (__ballot(mode != MODE_DONE) == 0) break;
     }
     cnt.rays = rays;
-    cnt.primary = __lane_id() == 0 ? queue.wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
-    trace_persistent_wave(P, queue, rt_start);
-    queue_release(P);
+    wave_pixels += queue.wave_pixels;
+    cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
+    trace_persistent_wave(P, queue, rt_start, wave_pixels);
+    if constexpr (GROUP) {
+        // one device-scope arrival per workgroup, by its last wave (an LDS count): 4 096 waves ending within tens of
+        // microseconds serialised on the one finished-waves word (~12 ns each, MI355X_MICROARCH.md fan-in)
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+        uint32_t fin = 0u;
+        if (__lane_id() == leader) fin = __hip_atomic_fetch_add(share_next + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        fin = __builtin_amdgcn_readlane(fin, leader);
+        if (fin == (blockDim.x >> 6) - 1u) queue_release(P, gridDim.x);
+    } else {
+        queue_release(P, grid_waves());
+    }
     flush_counts<COUNT_TESTS>(P, cnt);
 }
 
@@ -3247,17 +3354,30 @@ constexpr int kPhiloxCompactWaves = 8;  // ... of the non-texture Philox build o
 
 constexpr int kFlatWaves = 8;  // __launch_bounds__ waves per SIMD of the untextured flat kernel
 constexpr int kFlatPersistentWaves = 4;  // resident waves per SIMD of the persistent flat kernel's grid
+// RT_TUNE_PERSISTENT_GROUP: the persistent flat kernel's 16-wave workgroups with static tile shares (1, default) or
+// the round-5 one-wave workgroups on the per-wave queue alone (0)
+thread_local int g_persistent_group = 1;
+// RT_TUNE_GROUP_TAIL: permille of the frame's tiles left to the per-wave queue behind the groups' static shares
+thread_local int g_group_tail = 0;
+// RT_TUNE_GROUP_ORDER: the shares' tiles interleaved (0: tile g + k·groups) or in golden-ratio order (1)
+thread_local int g_group_order = 0;
+// RT_TUNE_QUEUE_RESET: 1 = rt_render zeroes the persistent kernels' queue slot per launch (and they skip queue_release)
+thread_local int g_queue_host_reset = 0;
+template <bool PH, bool G>
+KernelFn flat_persistent_pick(bool count, bool tex, bool trace) {
+    if (tex)
+        return count   ? dev::render_kernel_flat_persistent<true, true, PH, 1, false, G>
+               : trace ? dev::render_kernel_flat_persistent<false, true, PH, 1, true, G>
+                       : dev::render_kernel_flat_persistent<false, true, PH, 1, false, G>;
+    return count   ? dev::render_kernel_flat_persistent<true, false, PH, 1, false, G>
+           : trace ? dev::render_kernel_flat_persistent<false, false, PH, 1, true, G>
+                   : dev::render_kernel_flat_persistent<false, false, PH, 1, false, G>;
+}
 template <bool PH>
 KernelFn flat_pick(bool count, bool tex, bool persistent, bool trace) {
-    if (persistent) {
-        if (tex)
-            return count   ? dev::render_kernel_flat_persistent<true, true, PH, 1>
-                   : trace ? dev::render_kernel_flat_persistent<false, true, PH, 1, true>
-                           : dev::render_kernel_flat_persistent<false, true, PH, 1>;
-        return count   ? dev::render_kernel_flat_persistent<true, false, PH, 1>
-               : trace ? dev::render_kernel_flat_persistent<false, false, PH, 1, true>
-                       : dev::render_kernel_flat_persistent<false, false, PH, 1>;
-    }
+    if (persistent)
+        return g_persistent_group ? flat_persistent_pick<PH, true>(count, tex, trace)
+                                  : flat_persistent_pick<PH, false>(count, tex, trace);
     if (tex) return count ? dev::render_kernel_flat<true, true, PH, 1> : dev::render_kernel_flat<false, true, PH, 1>;
     return count ? dev::render_kernel_flat<true, false, PH, 1> : dev::render_kernel_flat<false, false, PH, kFlatWaves>;
 }
@@ -3688,6 +3808,42 @@ int rt_set_tuning(int key, int value) {
         g_prefetch_stop = value;
         return prev;
     }
+    if (key == RT_TUNE_PERSISTENT_GROUP) {
+        if (value < 0 || value > 1) {
+            set_error("rt_set_tuning: persistent group must be 0 or 1");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_persistent_group;
+        g_persistent_group = value;
+        return prev;
+    }
+    if (key == RT_TUNE_QUEUE_RESET) {
+        if (value < 0 || value > 1) {
+            set_error("rt_set_tuning: queue reset must be 0 or 1");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_queue_host_reset;
+        g_queue_host_reset = value;
+        return prev;
+    }
+    if (key == RT_TUNE_GROUP_ORDER) {
+        if (value < 0 || value > 1) {
+            set_error("rt_set_tuning: group order must be 0 or 1");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_group_order;
+        g_group_order = value;
+        return prev;
+    }
+    if (key == RT_TUNE_GROUP_TAIL) {
+        if (value < 0 || value > 1000) {
+            set_error("rt_set_tuning: group tail must be in [0, 1000] permille");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_group_tail;
+        g_group_tail = value;
+        return prev;
+    }
     if (key == RT_TUNE_FLAT_MAX) {
         if (value < 0 || value > (int)kFlatMaxPrims) {
             set_error("rt_set_tuning: flat kernel primitive limit must be in [0, 64]");
@@ -3961,8 +4117,11 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
                                         (size_t)(S.depth + 2) * 64 * (wide ? 4 : 2) + (size_t)g_lds_pad
                                   : 0;
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
+    // the persistent flat kernel's GROUP build: 16-wave workgroups (one per CU) whose share counter follows the tables
+    const bool group = V.kernel == 6 && g_persistent_group != 0;
+    const uint32_t block = group ? 1024u : (uint32_t)V.block;
     size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes +
-                       (V.kernel == 6 ? flat_tab_bytes : 0);
+                       (V.kernel == 6 ? flat_tab_bytes + (group ? 16u : 0u) : 0);  // (GROUP: 2 LDS words)
     if (lds_bytes > kLdsLimit) {
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
@@ -3991,24 +4150,59 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         int rc = hip_check(hipGetDevice(&device), "rt_render: hipGetDevice");
         if (rc == RT_OK) rc = acquire_queue(device, (uint32_t)g_queue_stride, &P.work_counter, &cus);
         if (rc == RT_OK)
-            rc = hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, V.block, lds_bytes),
+            rc = hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, block, lds_bytes),
                            "rt_render: occupancy query");
         if (rc != RT_OK) return rc;
+        if (group && per_cu > 1) {
+            // two 16-wave groups would fit a CU by registers: claim over half the CU's LDS so that the 1-per-CU grid
+            // below cannot put two groups on one CU and leave another empty
+            lds_bytes = std::max(lds_bytes, kLdsLimit / 2u + 1024u);
+            rc = hip_check(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes),
+                           "rt_render: LDS size attribute");
+            if (rc != RT_OK) return rc;
+        }
         P.work_total = tiles * 64u;
         P.pixel_cost = g_pixel_cost_bytes >= (uint64_t)P.work_total ? g_pixel_cost : nullptr;
         P.work_chunk = (uint32_t)g_queue_chunk;
         P.queue_prefetch = (uint32_t)g_queue_prefetch;
         P.queue_min = (uint32_t)g_queue_min;
         P.queue_stride = (uint32_t)g_queue_stride / 4u;
-        P.work_per_counter = (tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
+        // GROUP: the groups' static shares cover the first tiles, the per-wave queue the last g_group_tail permille
+        const uint32_t tail_tiles = group ? (uint32_t)(((uint64_t)tiles * (uint32_t)g_group_tail + 999u) / 1000u) : tiles;
+        P.group_tiles = tiles - tail_tiles;
+        P.queue_base = P.group_tiles * 64u;
+        P.work_per_counter = (tail_tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
         // the persistent flat kernel runs 4 waves per SIMD even where its registers allow 5-6: C5 0.294 vs 0.307 ms
         // (XORWOW), 0.300 vs 0.314 (Philox), 3 rounds on one box (profiles/r04f_ab_pflat_waves.txt)
-        if (V.kernel == 6) per_cu = std::min(per_cu, kFlatPersistentWaves * 4 * 64 / V.block);
-        if (g_persistent_waves > 0) per_cu = g_persistent_waves * 4 * 64 / V.block;
+        if (V.kernel == 6) per_cu = std::min(per_cu, std::max(1, kFlatPersistentWaves * 4 * 64 / (int)block));
+        if (g_persistent_waves > 0) per_cu = std::max(1, g_persistent_waves * 4 * 64 / (int)block);
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
+        if (group) grid = (tiles + block / 64u - 1u) / (block / 64u);  // (no more waves than tiles, as one-wave grids)
         grid = (uint32_t)(resident < grid ? resident : grid);
+        // GROUP shares in golden-ratio order (RT_TUNE_GROUP_ORDER 1): share g holds tiles (j · A) mod S for j in
+        // [g·K, g·K + K), A ≈ 0.618 S coprime with S — every share (and every XCD's) a spread sample of the frame, and
+        // the tiles the groups render at one moment scattered over it, not one band or one comb of tile columns
+        P.group_perm_a = P.group_perm_b = P.group_perm_k = 0u;
+        const uint64_t S = P.group_tiles;
+        if (group && g_group_order == 1 && S > 1u) {
+            const uint64_t K = (S + grid - 1u) / grid;
+            uint64_t A = (uint64_t)((double)S * 0.6180339887498949) | 1u;
+            while (std::gcd(A, S) != 1u) A++;
+            if ((uint64_t)(grid - 1u) * (S - 1u) + (K - 1u) * (S - 1u) < (1ull << 32)) {
+                P.group_perm_a = (uint32_t)A;
+                P.group_perm_b = (uint32_t)(K * A % S);
+                P.group_perm_k = (uint32_t)K;
+            }
+        }
         P.queue_guide = g_queue_guide > 0 ? std::max(1u, grid / dev::kQueueCounters) * (uint32_t)g_queue_guide : 0u;
-        // (no reset here: the slot is zero, the previous launch that used it left it so, queue_release)
+        // (no reset here: the slot is zero, the previous launch that used it left it so, queue_release — unless
+        // RT_TUNE_QUEUE_RESET asks for the round-4 host memset)
+        P.queue_host_reset = g_queue_host_reset ? 1u : 0u;
+        if (g_queue_host_reset) {
+            int rc2 = hip_check(hipMemsetAsync(P.work_counter, 0, (size_t)(dev::kQueueCounters + 2u) * P.queue_stride * 4u, s),
+                                "rt_render: queue reset");
+            if (rc2 != RT_OK) return rc2;
+        }
     }
     P.num_tiles = tiles;
     std::shared_ptr<TilePlan> plan;
@@ -4029,7 +4223,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     g_last_variant = variant;
     if (trial) (void)hipEventRecord(trial->ev[trial_slot], s);
     (void)hipGetLastError();
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(V.block), lds_bytes, s, P);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(block), lds_bytes, s, P);
     int rc = hip_check(hipGetLastError(), "rt_render: kernel launch", RT_ERR_LAUNCH);
     // A persistent launch that did not run leaves its queue slot as it found it, but the slot is re-zeroed anyway, so
     // that the launch reusing it kQueueSlots launches later never finds exhausted heads (the slot is

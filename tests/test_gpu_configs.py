@@ -571,4 +571,5 @@ def test_persistent_wave_trace_accounts_for_every_pixel(variant, c5_scene):
     xcc = (t[:, 4] >> 32) & 0xF
     assert set(np.unique(xcc).tolist()) <= set(range(8))
     grabs = t[:, 6] & 0xFFFFFFFF
-    assert int(grabs.sum()) * 128 >= cfg.width * cfg.height  # (a grab takes at most RT_TUNE_QUEUE_CHUNK = 128 indices)
+    if variant == 4:  # (variant 6 hands most pixels out of its workgroups' static shares, not by queue grabs)
+        assert int(grabs.sum()) * 128 >= cfg.width * cfg.height  # (a grab takes at most RT_TUNE_QUEUE_CHUNK = 128 indices)

@@ -1027,3 +1027,38 @@ def test_trace_rays_matches_brute_force_closest_hit():
         assert int(cnt[0]) == n and int(cnt[1]) > 2 * n
     assert np.isfinite(best).mean() > 0.3
 
+
+
+# (RT_TUNE_PERSISTENT_GROUP, RT_TUNE_GROUP_TAIL, RT_TUNE_GROUP_ORDER, RT_TUNE_QUEUE_RESET)
+GROUP_KNOBS = [(1, 0, 0, 0), (1, 0, 1, 0), (1, 100, 0, 0), (1, 1000, 0, 0), (1, 300, 1, 1), (0, 0, 0, 0), (0, 0, 0, 1)]
+
+
+@pytest.mark.parametrize("group, tail, order, reset", GROUP_KNOBS, ids=lambda v: str(v))
+def test_persistent_flat_group_knobs_change_schedule_not_pixels(group, tail, order, reset):
+    """The persistent flat kernel's workgroup shares (round 6): 16-wave groups handing a static share of the tiles to
+    their lanes through an LDS counter, the per-wave queue behind them (RT_TUNE_GROUP_TAIL permille of the tiles), the
+    shares' order, and the queue slot's reset (in-kernel by the last group or wave, or a host memset) decide which lane
+    renders which pixel, never what it computes: every setting gives the golden image, ray count and RNG states, on a
+    textured scene (C5's) and on the Cornell box, frame after frame on the reused queue slots."""
+    keys = (abi.RT_TUNE_PERSISTENT_GROUP, abi.RT_TUNE_GROUP_TAIL, abi.RT_TUNE_GROUP_ORDER, abi.RT_TUNE_QUEUE_RESET)
+    prev = [lib().rt_set_tuning(k, v) for k, v in zip(keys, (group, tail, order, reset))]
+    assert min(prev) >= 0
+    lib().rt_set_variant(6)
+    try:
+        for name in ("c5_textured_160x96_s4", "c3_cornell_128_s16"):
+            case = CASE_BY_NAME[name]
+            cfg, g = case.cfg(), load_golden(case.name)
+            ds = DeviceScene(scenes.builtin(cfg.scene))
+            for _ in range(2):
+                r = Renderer(cfg.width, cfg.height)
+                r.render_init()
+                r.render(ds, cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
+                torch.cuda.synchronize()
+                assert lib().rt_last_variant() == 6
+                np.testing.assert_array_equal(r.image(), g["pos"], err_msg=name)
+                assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes(), name
+                assert int(r.counters[0]) == int(g["counters"][0]), name
+    finally:
+        lib().rt_set_variant(-1)
+        for k, v in zip(keys, prev):
+            lib().rt_set_tuning(k, v)
