@@ -37,6 +37,7 @@ RT_TUNE_PREFETCH_STOP = 17
 RT_TUNE_PERSISTENT_GROUP = 18  # persistent flat kernel: 16-wave workgroups with static tile shares (1) or not (0)
 RT_TUNE_GROUP_ORDER = 20  # ... the shares' tiles interleaved (0) or in golden-ratio order (1)
 RT_TUNE_QUEUE_RESET = 21  # 1 = rt_render memsets the persistent queue slot per launch
+RT_TUNE_GROUP_CHUNK = 22  # ... positions per chunk of the workgroup chunk queue (group mode 2)
 RT_TUNE_GROUP_TAIL = 19  # ... permille of the tiles left to the per-wave queue behind the shares
 
 STATUS = {

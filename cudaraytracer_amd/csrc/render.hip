@@ -270,6 +270,7 @@ struct KParams {
     uint32_t group_perm_a;           // GROUP: 0 = interleaved shares; else the shares' golden-ratio step (GroupShare)
     uint32_t group_perm_b, group_perm_k;  // ... (group_perm_k · group_perm_a) mod group_tiles, and tiles per share
     uint32_t queue_host_reset;       // persistent kernels: 1 = rt_render zeroed the queue slot (no queue_release)
+    uint32_t group_chunk;            // ... positions per chunk (a multiple of 64)
 };
 
 constexpr int kStackMax = 64;
@@ -2994,6 +2995,121 @@ struct GroupShare {
     }
 };
 
+// The persistent flat kernel's workgroup chunk queue (GROUP 2: RT_TUNE_PERSISTENT_GROUP 2, the default since round
+// 6).  Static shares leave the load balance to the shares' sizes, but the XCDs of one MI355X do not render at one
+// speed (equal shares ended 196-253 us per XCD, profiles/r06b_ab_c5_group_shares.txt).  Here a workgroup draws chunks
+// of tiles from the frame's queue heads (one device atomic per chunk and group, not per wave) and hands their positions
+// to its lanes through its LDS counter.  Chunk c covers positions [c·C, c·C + C) (C = P.group_chunk); it is fetched
+// by the wave whose claim holds the first position of chunk c - kGqAhead (chunks 0 .. kGqAhead - 1 by thread 0 at the
+// start), in chunk order (a fetch waits for the previous chunk's slot), so a chunk that comes back empty means every
+// later one is empty too, and every position of a non-empty chunk has been claimed by then.  A lane resolves the
+// position it claimed from its chunk's slot in an LDS ring of kGqRing (waiting for the slot if its fetch is in
+// flight); positions past a partial chunk's valid indices are claimed again.  Near the end of a head the chunks shrink
+// (guided by the indices the head had left at the group's last fetch).
+constexpr uint32_t kGqRing = 16;   // chunk slots in LDS (a slot is reused kGqRing chunks later)
+constexpr uint32_t kGqAhead = 2;   // chunks fetched ahead of the one being handed out
+constexpr uint32_t kGqWords = 8 + 4 * kGqRing;
+// LDS words from w: [0] positions claimed, [1] head the group draws from, [2] indices that head had left at the
+// group's last fetch; slot s at [8 + 4s]: tag (chunk id + 1; 0 = empty), first work index, valid indices
+struct GroupQueue {
+    uint32_t* w;
+    bool done = false;  // wave-uniform: a chunk came back empty (the frame's queue is exhausted)
+    __device__ explicit GroupQueue(uint32_t* lds) : w(lds) {}
+    __device__ static uint32_t lds_load(const uint32_t* a) {
+        return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ static void lds_store(uint32_t* a, uint32_t v) {
+        __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // one lane: the next chunk's indices from the group's head — guided near the head's end — moving on to the next
+    // live head when it is exhausted.  Returns (first index, count), count 0 once every head is exhausted.
+    __device__ static uint2 fetch(const KParams& P, uint32_t* w) {
+        uint32_t qc = lds_load(w + 1);
+        const uint32_t left = lds_load(w + 2), per_head = max(1u, gridDim.x / kQueueCounters);
+        const uint32_t want = min(P.group_chunk, max(64u, (left / (2u * per_head)) & ~63u));
+        for (uint32_t tries = 0; tries <= kQueueCounters; tries++) {
+            const uint32_t b = atomicAdd(P.work_counter + qc * P.queue_stride, want);
+            const uint32_t idx = P.queue_base + qc * P.work_per_counter + b;
+            if (b < P.work_per_counter && idx < P.work_total) {
+                const uint32_t n = min(want, min(P.work_per_counter - b, P.work_total - idx));
+                lds_store(w + 1, qc);
+                lds_store(w + 2, P.work_per_counter - b - min(want, P.work_per_counter - b));
+                return make_uint2(idx, n);
+            }
+            const uint32_t done = atomicOr(P.work_counter + kQueueCounters * P.queue_stride, 1u << qc) | (1u << qc);
+            if (done == kQueueAllDone) break;
+            const uint32_t live = ~done & kQueueAllDone, above = live & ~((2u << qc) - 1u);
+            qc = (uint32_t)__builtin_ctz(above ? above : live);
+            lds_store(w + 2, 0xffffffffu);  // (a new head: its remaining count is not known yet)
+        }
+        lds_store(w + 1, qc);
+        return make_uint2(0u, 0u);
+    }
+    __device__ static void publish(uint32_t* w, uint32_t chunk, uint2 r) {
+        uint32_t* slot = w + 8 + 4 * (chunk % kGqRing);
+        lds_store(slot + 1, r.x);
+        lds_store(slot + 2, r.y);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot's words before its tag
+        __hip_atomic_store(slot, chunk + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // thread 0, before the kernel's first barrier
+    __device__ static void init(const KParams& P, uint32_t* w) {
+        w[0] = 0u;
+        w[1] = blockIdx.x % kQueueCounters;
+        w[2] = 0xffffffffu;
+        for (uint32_t s = 0; s < kGqRing; s++) w[8 + 4 * s] = 0u;
+        for (uint32_t c = 0; c < kGqAhead; c++) publish(w, c, fetch(P, w));
+    }
+    // Lanes with `need` claim positions (ballot + mbcnt rank) and start(x, g, pix, idx) runs on every lane that gets a
+    // pixel.  A lane still needing one afterwards found the frame's queue exhausted (done).
+    template <class F>
+    __device__ __forceinline__ uint32_t take(const KParams& P, bool& need, F&& start) {
+        uint64_t needm = __ballot(need);
+        uint32_t taken_px = 0u;
+        const uint32_t C = P.group_chunk;
+        while (needm != 0 && !done) {
+            const uint32_t k = (uint32_t)__popcll(needm);
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)needm) - 1u;
+            uint32_t p = 0u;
+            if (__lane_id() == leader) p = __hip_atomic_fetch_add(w, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p = __builtin_amdgcn_readlane(p, leader);
+            const uint32_t cs = (p + C - 1u) / C;  // the first chunk starting at or after p
+            if (cs * C < p + k && __lane_id() == leader) {  // this claim holds chunk cs's first position
+                const uint32_t j = cs + kGqAhead;
+                while (lds_load(w + 8 + 4 * ((j - 1u) % kGqRing)) < j) __builtin_amdgcn_s_sleep(1);  // chunk j - 1 first
+                publish(w, j, fetch(P, w));
+            }
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+            bool dry = false;
+            if (need && rank < k) {
+                const uint32_t pos = p + rank, c = pos / C, off = pos - c * C;
+                const uint32_t* slot = w + 8 + 4 * (c % kGqRing);
+                // (its fetch is in flight; the slot is reused only kGqRing chunks later, far beyond any claim)
+                while (__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c + 1u)
+                    __builtin_amdgcn_s_sleep(1);
+                const uint32_t first = lds_load(slot + 1), cnt = lds_load(slot + 2);
+                if (cnt == 0u) {
+                    dry = true;
+                } else if (off < cnt) {
+                    uint32_t x, g, pix;
+                    if (work_pixel(P, first + off, x, g, pix)) {
+                        need = false;
+                        start(x, g, pix, first + off);
+                    }
+                }
+            }
+            if (__ballot(dry) != 0) done = true;
+            const uint64_t still = __ballot(need);
+            taken_px += (uint32_t)__popcll(needm & ~still);
+            needm = still;
+        }
+        return taken_px;
+    }
+    // indices the group's head had left at its last fetch (0xffffffff: unknown)
+    __device__ uint32_t head_left() const { return lds_load(w + 2); }
+};
+
 // Persistent flat kernel (variant 6): the flat kernel's closest-hit query in v4's persistent grid — a device-filling
 // grid whose lanes take the next pixel from the frame's work queue as soon as theirs is done (PixelQueue), for frames
 // with few samples per pixel (BASELINE config 5: 1 spp), where a tile wave would idle on its slowest pixels.  The path
@@ -3008,9 +3124,11 @@ struct GroupShare {
 // queue_release, which leaves the queue slot zeroed for its next user.
 constexpr int kFlatPrefetch = 1;
 constexpr uint32_t kPrefetchStop = 8;
-// GROUP (round 6, the default): 1024-thread workgroups, one per CU, whose waves draw from the group's static share
-// first (GroupShare) and from the per-wave queue after it; !GROUP: one-wave workgroups on the per-wave queue alone.
-template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD, bool TRACE = false, bool GROUP = true>
+// GROUP (RT_TUNE_PERSISTENT_GROUP, round 6): 2 (the default) — 1024-thread workgroups, one per CU, drawing chunks of
+// tiles from the queue heads for their lanes (GroupQueue); 1 — the same workgroups handing out a static share of the
+// tiles (GroupShare), then the per-wave queue over the tiles past the shares; 0 — one-wave workgroups on the per-wave
+// queue alone (round 5).  Each build carries only its own scheduling code.
+template <bool COUNT_TESTS, bool TEX, bool PHILOX, int WAVES_PER_SIMD, bool TRACE = false, int GROUP = 2>
 __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kernel_flat_persistent(const KParams P) {
     using R = typename std::conditional<PHILOX, RngPhilox, Rng>::type;
     constexpr bool kNext = (kFlatPrefetch & 1) && !PHILOX;  // (Philox has no per-pixel state to load)
@@ -3039,6 +3157,7 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
         for (uint32_t i = tid; i < 3u * P.num_mats; i += nt) tmats[i] = P.mats[i];
         for (uint32_t i = tid; i < P.num_imgs; i += nt) timgs[i] = P.imgs[i];
         if (GROUP && tid < 2u) share_next[tid] = 0u;  // (the share's counter, the group's finished waves)
+        if (GROUP == 2 && tid == 0u) GroupQueue::init(P, share_next + 2);
         __syncthreads();
     }
     Counts cnt{0, 0, 0, 0, 0, 0, 0};
@@ -3056,15 +3175,20 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
     const uint32_t wave_id = grid_wave_id(), n_waves = grid_waves();
     PixelQueue<TRACE> queue(wave_id % kQueueCounters);
     GroupShare share(P, share_next);
-    if (!GROUP) share.done = true;
-    if (P.work_per_counter == 0u) queue.drained = true;  // (GROUP with no tail: every tile is in the shares)
+    if (GROUP != 1) share.done = true;
+    // (GROUP 1 with no tail: every tile is in the shares; GROUP 2: the workgroups draw the queue themselves)
+    if (GROUP == 2 || P.work_per_counter == 0u) queue.drained = true;
+    GroupQueue gq(share_next + 2);
+    if (GROUP != 2) gq.done = true;
     uint32_t wave_pixels = 0u;  // pixels this wave took from its group's share
     const uint64_t rt_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0u;
     // pass trace (diagnostic, tools/c5_tail.py): every 64th wave stamps each of its first kPassTrace / 4 passes with 4
     // words: s_memrealtime at the pass start (bits 0-39) with the lanes about to trace (40-46), shade (47-53) and with a
     // pixel at all (54-60); then s_memrealtime after the trace, after the shading and after the queue
     constexpr uint32_t kPassTrace = 1024;
-    const bool pass_traced = TRACE && P.wave_trace && (wave_id & 63u) == 0u &&
+    // (one wave of every 64 consecutive wave ids, at a different offset in each block: in 16-wave groups every wave
+    // index of a group is sampled, not only each group's first wave)
+    const bool pass_traced = TRACE && P.wave_trace && (wave_id & 63u) == ((wave_id >> 6) * 17u & 63u) &&
                              (uint64_t)P.wave_trace_words >= (uint64_t)kWaveTraceWords * n_waves +
                                  (uint64_t)kPassTrace * (wave_id / 64u + 1u);
     unsigned long long* const pass_rec =
@@ -3143,12 +3267,18 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
             const auto start_new = [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {  // Kernel.cu:119-123
                 start(qx, qg, qpix, qidx, begin_rng<R>(state_at(P, qpix), P.state_stride, qg * P.width + qx));
             };
-            if (GROUP && !share.done) {
+            if (GROUP == 1 && !share.done) {
                 const uint32_t n = share.take(P, need, start_new);
                 wave_pixels += n;
                 if (TRACE && n) queue.rt_last = __builtin_amdgcn_s_memrealtime();  // (last pixel handed out)
             }
-            if (__ballot(need) != 0) queue.take(P, need, start_new);
+            if (GROUP == 2 && !gq.done) {
+                const uint32_t n = gq.take(P, need, start_new);
+                wave_pixels += n;
+                if (TRACE && n) queue.rt_last = __builtin_amdgcn_s_memrealtime();
+                if (TRACE && gq.done && !queue.rt_drained) queue.rt_drained = __builtin_amdgcn_s_memrealtime();
+            }
+            if (GROUP != 2 && __ballot(need) != 0) queue.take(P, need, start_new);
             if (need) mode = MODE_DONE;
             if constexpr (kNext) {  // the next pixel of every lane that just started one: its state loads go out now
                 const auto take_next = [&](uint32_t qx, uint32_t qg, uint32_t qpix, uint32_t qidx) {
@@ -3161,9 +3291,12 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
                 // (from the group's share while it holds more than 1/prefetch_stop of itself; then from the queue by
                 // the same rule on the wave's head)
                 bool want = started && npix == kNone && P.prefetch_stop != 0u;
-                if (GROUP && !share.done) {
+                if (GROUP == 1 && !share.done) {
                     want = want && share.left > share.total / P.prefetch_stop;
                     if (__ballot(want) != 0) wave_pixels += share.take(P, want, take_next);
+                } else if (GROUP == 2) {
+                    want = want && !gq.done && gq.head_left() > P.work_per_counter / P.prefetch_stop;
+                    if (__ballot(want) != 0) wave_pixels += gq.take(P, want, take_next);
                 } else {
                     want = want && queue.head_left > P.work_per_counter / P.prefetch_stop;
                     if (__ballot(want) != 0) queue.take(P, want, take_next);
@@ -3354,16 +3487,19 @@ constexpr int kPhiloxCompactWaves = 8;  // ... of the non-texture Philox build o
 
 constexpr int kFlatWaves = 8;  // __launch_bounds__ waves per SIMD of the untextured flat kernel
 constexpr int kFlatPersistentWaves = 4;  // resident waves per SIMD of the persistent flat kernel's grid
-// RT_TUNE_PERSISTENT_GROUP: the persistent flat kernel's 16-wave workgroups with static tile shares (1, default) or
-// the round-5 one-wave workgroups on the per-wave queue alone (0)
-thread_local int g_persistent_group = 1;
+// RT_TUNE_PERSISTENT_GROUP: the persistent flat kernel's 16-wave workgroups drawing chunks from the queue heads (2,
+// default: GroupQueue), with static tile shares (1: GroupShare), or the round-5 one-wave workgroups on the per-wave
+// queue alone (0); profiles/r06b_ab_c5_group_shares.txt
+thread_local int g_persistent_group = 2;
 // RT_TUNE_GROUP_TAIL: permille of the frame's tiles left to the per-wave queue behind the groups' static shares
 thread_local int g_group_tail = 0;
 // RT_TUNE_GROUP_ORDER: the shares' tiles interleaved (0: tile g + k·groups) or in golden-ratio order (1)
 thread_local int g_group_order = 0;
+// RT_TUNE_GROUP_CHUNK: positions per chunk of the workgroup chunk queue (RT_TUNE_PERSISTENT_GROUP 2)
+thread_local int g_group_chunk = 1024;
 // RT_TUNE_QUEUE_RESET: 1 = rt_render zeroes the persistent kernels' queue slot per launch (and they skip queue_release)
 thread_local int g_queue_host_reset = 0;
-template <bool PH, bool G>
+template <bool PH, int G>
 KernelFn flat_persistent_pick(bool count, bool tex, bool trace) {
     if (tex)
         return count   ? dev::render_kernel_flat_persistent<true, true, PH, 1, false, G>
@@ -3376,8 +3512,9 @@ KernelFn flat_persistent_pick(bool count, bool tex, bool trace) {
 template <bool PH>
 KernelFn flat_pick(bool count, bool tex, bool persistent, bool trace) {
     if (persistent)
-        return g_persistent_group ? flat_persistent_pick<PH, true>(count, tex, trace)
-                                  : flat_persistent_pick<PH, false>(count, tex, trace);
+        return g_persistent_group == 2 ? flat_persistent_pick<PH, 2>(count, tex, trace)
+               : g_persistent_group == 1 ? flat_persistent_pick<PH, 1>(count, tex, trace)
+                                         : flat_persistent_pick<PH, 0>(count, tex, trace);
     if (tex) return count ? dev::render_kernel_flat<true, true, PH, 1> : dev::render_kernel_flat<false, true, PH, 1>;
     return count ? dev::render_kernel_flat<true, false, PH, 1> : dev::render_kernel_flat<false, false, PH, kFlatWaves>;
 }
@@ -3808,9 +3945,18 @@ int rt_set_tuning(int key, int value) {
         g_prefetch_stop = value;
         return prev;
     }
+    if (key == RT_TUNE_GROUP_CHUNK) {
+        if (value < 64 || value > 4096 || value % 64) {
+            set_error("rt_set_tuning: group chunk must be a multiple of 64 in [64, 4096]");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_group_chunk;
+        g_group_chunk = value;
+        return prev;
+    }
     if (key == RT_TUNE_PERSISTENT_GROUP) {
-        if (value < 0 || value > 1) {
-            set_error("rt_set_tuning: persistent group must be 0 or 1");
+        if (value < 0 || value > 2) {
+            set_error("rt_set_tuning: persistent group must be 0, 1 or 2");
             return RT_ERR_INVALID_ARGUMENT;
         }
         int prev = g_persistent_group;
@@ -4112,6 +4258,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // a visit at level L (root = 1) holds at most L - 1 deferred children, so its unconditional write of
     // the far child lands at index 2 + (L - 1) <= depth + 1 (the 128-B saving keeps config 2's wave
     // inside 10 × 512 B of LDS)
+    const int group_mode = V.kernel == 6 ? g_persistent_group : 0;
     const size_t wave_bytes = V.stack == dev::STACK_LDS16
                                   ? (size_t)(persistent ? dev::PK_WORDS4 : dev::park_words(V.compact)) * 64 * 4 +
                                         (size_t)(S.depth + 2) * 64 * (wide ? 4 : 2) + (size_t)g_lds_pad
@@ -4121,7 +4268,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     const bool group = V.kernel == 6 && g_persistent_group != 0;
     const uint32_t block = group ? 1024u : (uint32_t)V.block;
     size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes +
-                       (V.kernel == 6 ? flat_tab_bytes + (group ? 16u : 0u) : 0);  // (GROUP: 2 LDS words)
+                       (V.kernel == 6 ? flat_tab_bytes + (group ? 4u * (2u + dev::kGqWords) : 0u) : 0);  // (GROUP)
     if (lds_bytes > kLdsLimit) {
         set_error("rt_render: BVH too deep for the LDS stack of kernel variant " + std::to_string(variant));
         return RT_ERR_UNSUPPORTED;
@@ -4168,7 +4315,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.queue_min = (uint32_t)g_queue_min;
         P.queue_stride = (uint32_t)g_queue_stride / 4u;
         // GROUP: the groups' static shares cover the first tiles, the per-wave queue the last g_group_tail permille
-        const uint32_t tail_tiles = group ? (uint32_t)(((uint64_t)tiles * (uint32_t)g_group_tail + 999u) / 1000u) : tiles;
+        const uint32_t tail_tiles =
+            group && group_mode == 1 ? (uint32_t)(((uint64_t)tiles * (uint32_t)g_group_tail + 999u) / 1000u) : tiles;
+        P.group_chunk = (uint32_t)g_group_chunk;
         P.group_tiles = tiles - tail_tiles;
         P.queue_base = P.group_tiles * 64u;
         P.work_per_counter = (tail_tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;

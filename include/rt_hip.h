@@ -406,8 +406,9 @@ int rt_last_variant(void);
  *   take their next pixel (and its RNG state) ahead while their wave's queue head holds more than 1/value of its
  *   range (default 8; 0 = never ahead; 0..1024).  RT_TUNE_PERSISTENT_GROUP: the persistent flat kernel runs 16-wave
  *   workgroups, one per CU, each handing a static interleaved share of the frame's tiles to its lanes through an LDS
- *   counter before its waves turn to the per-wave queue (1, default; round 6), or one-wave workgroups on the queue
- *   alone (0, round 5).  RT_TUNE_GROUP_TAIL: permille of the frame's tiles left to the per-wave queue behind the
+ *   counter before its waves turn to the per-wave queue (1; round 6), or one-wave workgroups on the queue alone (0,
+ *   round 5), or 16-wave workgroups drawing chunks of RT_TUNE_GROUP_CHUNK positions (64..4096, default 1024) from the
+ *   queue heads themselves, one device atomic per chunk and group (2, default).  RT_TUNE_GROUP_TAIL: permille of the frame's tiles left to the per-wave queue behind the
  *   shares (0..1000, default 0).  RT_TUNE_GROUP_ORDER: the shares' tiles interleaved (0, default: tile g + k·groups) or in
  *   golden-ratio order (1: share g holds tiles (j · A) mod S, j in [g·K, g·K + K)).  None of these changes
  *   the image.  RT_TUNE_QUEUE_RESET: 1 = rt_render zeroes the persistent kernels' work-queue slot with a memset per
@@ -419,7 +420,7 @@ enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_
                      RT_TUNE_FLAT_MAX = 12, RT_TUNE_QUEUE_PREFETCH = 13, RT_TUNE_QUEUE_GUIDE = 14,
                      RT_TUNE_QUEUE_MIN_CHUNK = 15, RT_TUNE_RIUS_TRIPS_PERSISTENT = 16, RT_TUNE_PREFETCH_STOP = 17,
                      RT_TUNE_PERSISTENT_GROUP = 18, RT_TUNE_GROUP_TAIL = 19, RT_TUNE_GROUP_ORDER = 20,
-                     RT_TUNE_QUEUE_RESET = 21 };
+                     RT_TUNE_QUEUE_RESET = 21, RT_TUNE_GROUP_CHUNK = 22 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

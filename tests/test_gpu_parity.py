@@ -1030,7 +1030,8 @@ def test_trace_rays_matches_brute_force_closest_hit():
 
 
 # (RT_TUNE_PERSISTENT_GROUP, RT_TUNE_GROUP_TAIL, RT_TUNE_GROUP_ORDER, RT_TUNE_QUEUE_RESET)
-GROUP_KNOBS = [(1, 0, 0, 0), (1, 0, 1, 0), (1, 100, 0, 0), (1, 1000, 0, 0), (1, 300, 1, 1), (0, 0, 0, 0), (0, 0, 0, 1)]
+GROUP_KNOBS = [(1, 0, 0, 0), (1, 0, 1, 0), (1, 100, 0, 0), (1, 1000, 0, 0), (1, 300, 1, 1), (0, 0, 0, 0), (0, 0, 0, 1),
+               (2, 0, 0, 0), (2, 0, 0, 1)]
 
 
 @pytest.mark.parametrize("group, tail, order, reset", GROUP_KNOBS, ids=lambda v: str(v))
@@ -1058,6 +1059,32 @@ def test_persistent_flat_group_knobs_change_schedule_not_pixels(group, tail, ord
                 np.testing.assert_array_equal(r.image(), g["pos"], err_msg=name)
                 assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes(), name
                 assert int(r.counters[0]) == int(g["counters"][0]), name
+    finally:
+        lib().rt_set_variant(-1)
+        for k, v in zip(keys, prev):
+            lib().rt_set_tuning(k, v)
+
+
+@pytest.mark.parametrize("chunk", [64, 128, 1024, 4096])
+def test_persistent_flat_group_queue_chunks(chunk):
+    """The workgroup chunk queue (RT_TUNE_PERSISTENT_GROUP 2): any chunk size — from one tile per chunk to chunks
+    larger than a small frame's share of a queue head — renders the golden image, rays and RNG states."""
+    keys = (abi.RT_TUNE_PERSISTENT_GROUP, abi.RT_TUNE_GROUP_CHUNK)
+    prev = [lib().rt_set_tuning(k, v) for k, v in zip(keys, (2, chunk))]
+    assert min(prev) >= 0
+    lib().rt_set_variant(6)
+    try:
+        for name in ("c5_textured_160x96_s4", "c3_cornell_128_s16"):
+            case = CASE_BY_NAME[name]
+            cfg, g = case.cfg(), load_golden(case.name)
+            r = Renderer(cfg.width, cfg.height)
+            r.render_init()
+            r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
+            torch.cuda.synchronize()
+            assert lib().rt_last_variant() == 6
+            np.testing.assert_array_equal(r.image(), g["pos"], err_msg=name)
+            assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes(), name
+            assert int(r.counters[0]) == int(g["counters"][0]), name
     finally:
         lib().rt_set_variant(-1)
         for k, v in zip(keys, prev):

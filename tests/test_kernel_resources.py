@@ -74,9 +74,9 @@ def test_hot_kernels_register_and_scratch_budget(tmp_path):
     assert meta[_v3(0, 1, 1)]["vgpr_count"] <= 64
 
 
-def _flat(t, p, persistent=False, trace=0, group=1):
-    if persistent:  # (GROUP = 1: 16-wave workgroups with static tile shares, the default; 0: round 5's one-wave form)
-        return f"_ZN2rt3dev29render_kernel_flat_persistentILb0ELb{t}ELb{p}ELi1ELb{trace}ELb{group}EEEvNS0_7KParamsE"
+def _flat(t, p, persistent=False, trace=0, group=2):
+    if persistent:  # (GROUP 2: 16-wave workgroups drawing chunks, the default; 1: static shares; 0: round 5's one-wave form)
+        return f"_ZN2rt3dev29render_kernel_flat_persistentILb0ELb{t}ELb{p}ELi1ELb{trace}ELi{group}EEEvNS0_7KParamsE"
     return f"_ZN2rt3dev18render_kernel_flatILb0ELb{t}ELb{p}ELi{8 if not t else 1}EEEvNS0_7KParamsE"
 
 
@@ -88,7 +88,7 @@ def test_flat_kernels_register_and_scratch_budget(tmp_path):
     meta = kernel_metadata(tmp_path)
     for t in (0, 1):
         for p in (0, 1):
-            for k in (_flat(t, p), _flat(t, p, True), _flat(t, p, True, group=0)):
+            for k in (_flat(t, p), _flat(t, p, True), _flat(t, p, True, group=1), _flat(t, p, True, group=0)):
                 assert k in meta, k
                 assert meta[k]["private_segment_fixed_size"] <= 192, (k, meta[k])
     assert meta[_flat(0, 0)]["vgpr_count"] <= 64
@@ -100,6 +100,8 @@ def test_flat_kernels_register_and_scratch_budget(tmp_path):
         for p in (0, 1):
             assert _flat(t, p, True, trace=1) in meta and _v4(t, p, trace=1) in meta
     assert meta[_flat(1, 0, True, group=0)]["sgpr_spill_count"] <= 40, meta[_flat(1, 0, True, group=0)]
-    # round 6: the GROUP build (the default) carries the share's state too; its wave id is read as an SGPR
-    # (readfirstlane) — computed per lane it put the queue's head index in VGPRs: 82 spills, 504 v_readlane
-    assert meta[_flat(1, 0, True)]["sgpr_spill_count"] <= 56, meta[_flat(1, 0, True)]
+    # round 6: the GROUP builds (2, the default: chunk queue; 1: static shares) each carry only their own scheduling
+    # code, and the wave id is read as an SGPR (readfirstlane) — computed per lane it had put the queue's head index in
+    # VGPRs: 82 spills, 504 v_readlane
+    assert meta[_flat(1, 0, True)]["sgpr_spill_count"] <= 32, meta[_flat(1, 0, True)]
+    assert meta[_flat(1, 0, True, group=1)]["sgpr_spill_count"] <= 56, meta[_flat(1, 0, True, group=1)]
