@@ -374,26 +374,39 @@ def run_rank(args) -> dict | None:
         dist.barrier()
     r.counters.zero_()
     stream = torch.cuda.current_stream()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # HIP events on the render stream.  N > 1: three per step (render, then the gather's share of the stream);
+    # N = 1: one pair around the K launches — every event record between two launches puts a marker packet between
+    # them (~11 us per C5 frame, 4 %, in round 5's ms_per_step), which a viewer's back-to-back frames do not have.
+    # kernel_ms is then the stream's time per frame, kernel plus the launch-to-launch gap (rocprofv3 agrees, §4).
+    per_step = world > 1
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps if per_step else 1)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    if not per_step:
+        ev[0][0].record(stream)
     for i in range(args.steps):
-        ev[i][0].record(stream)
+        if per_step:
+            ev[i][0].record(stream)
         r.render(scene, cfg.spp, cfg.depth, frame_inputs(), flags=frame_flags)
-        ev[i][1].record(stream)
-        if world > 1:
+        if per_step:
+            ev[i][1].record(stream)
             gatherer.start(r.pos)  # waits (stream-side) for frame i - 1's gather, then starts frame i's
-        ev[i][2].record(stream)
+            ev[i][2].record(stream)
+    if not per_step:
+        ev[0][1].record(stream)
     if world > 1:
         gatherer.finish()  # the last frame's gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
-    gather_ms = sum(b.elapsed_time(g) for _, b, g in ev) / args.steps
+    if per_step:
+        kernel_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
+        gather_ms = sum(b.elapsed_time(g) for _, b, g in ev) / args.steps
+    else:
+        kernel_ms, gather_ms = ev[0][0].elapsed_time(ev[0][1]) / args.steps, 0.0
     rays = int(r.counters[0].item())
     stats = torch.tensor([elapsed, kernel_ms, gather_ms], dtype=torch.float64, device=red_dev)
     tot = torch.tensor([rays, f_launch], dtype=torch.int64, device=red_dev)
