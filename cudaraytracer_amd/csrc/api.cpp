@@ -67,7 +67,8 @@ static void free_device(DeviceScene* s) {
     s->prims_flat = s->ref_nodes = s->flat_boxes = nullptr;
     if (s->bvh_ref_nodes) (void)hipFree((void*)s->bvh_ref_nodes);
     if (s->bvh_boxes) (void)hipFree((void*)s->bvh_boxes);
-    s->bvh_ref_nodes = s->bvh_boxes = nullptr;
+    if (s->bvh_ref_pairs) (void)hipFree((void*)s->bvh_ref_pairs);
+    s->bvh_ref_nodes = s->bvh_boxes = s->bvh_ref_pairs = nullptr;
     if (s->mats) (void)hipFree((void*)s->mats);
     if (s->imgs) (void)hipFree((void*)s->imgs);  // texels: owned by rt_scene::texel_block
     s->nodes = s->prims = s->mats = nullptr;
@@ -101,6 +102,8 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.bvh_ref_nodes = p;
     if ((rc = upload(h.bvh_boxes, &p, "hipMalloc/hipMemcpy(bvh_boxes)"))) goto fail;
     d.bvh_boxes = p;
+    if ((rc = upload(h.bvh_ref_pairs, &p, "hipMalloc/hipMemcpy(bvh_ref_pairs)"))) goto fail;
+    d.bvh_ref_pairs = p;
     d.flat_runs[0] = h.flat_runs[0];
     d.flat_runs[1] = h.flat_runs[1];
     if ((rc = upload(h.mats, &p, "hipMalloc/hipMemcpy(materials)"))) goto fail;
@@ -123,7 +126,7 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.has_textures = h.has_textures;
     d.has_rects = h.has_rects;
     d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs.size() + h.prims.size() + h.prims_flat.size() + h.ref_nodes.size() +
-                      h.flat_boxes.size() + h.bvh_ref_nodes.size() + h.bvh_boxes.size() + h.mats.size()) * 4 +
+                      h.flat_boxes.size() + h.bvh_ref_nodes.size() + h.bvh_boxes.size() + h.bvh_ref_pairs.size() + h.mats.size()) * 4 +
                      h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;

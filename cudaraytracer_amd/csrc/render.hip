@@ -263,6 +263,7 @@ struct KParams {
     uint32_t flat_runs[2];           // flat kernel: [begin, end) of each primitive type's run in the flat table
     const float4* bvh_ref_nodes;     // BVH kernels: the reference BVH over `prims` (bvh_clear), NULL = no replay
     const float4* bvh_boxes;         // BVH kernels: per `prims` record its reference box (bvh_clear)
+    const float4* bvh_ref_pairs;     // BVH kernels: per reference node its children's boxes and refs (ref_trace_wave)
     uint32_t bvh_has_rects;          // BVH kernels: the scene holds a rectangle (bvh_clear's check of misses)
     uint32_t prefetch_stop;          // persistent flat: next pixels are taken ahead while the head holds > 1/this (0: never)
     uint32_t group_tiles;            // persistent flat, GROUP: tiles [0, group_tiles) are the workgroups' static shares
@@ -639,7 +640,7 @@ __device__ __noinline__ void bvh_replay(PP P, const float4* __restrict__ prims, 
 
 // The reference traversal (ref_trace's algorithm and arithmetic) for one wave-uniform ray, without a call or private
 // memory: every value is uniform — node and primitive records are scalar loads, the tests' arithmetic runs on uniform
-// operands — and the stack lives across the lanes of two VGPRs (entry j in lane j, v_writelane / v_readlane at the
+// operands — and the stack lives across the lanes of one VGPR (entry j in lane j, v_writelane / v_readlane at the
 // uniform top; at most kRefTreeMaxDepthBvh + 1 < 64 entries).  Every lane of the wave must be active (v3 and v4 keep
 // all 64 lanes in their loops), so no copy of the stack registers can drop a lane.
 typedef const __attribute__((address_space(4))) float ConstF32R;
@@ -649,8 +650,12 @@ __device__ __forceinline__ uint32_t lane_write(uint32_t vec, const uint32_t val,
     asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(vec) : "s"(v), "{m0}"(l));
     return vec;
 }
-__device__ __forceinline__ HitOut ref_trace_wave(const float4* __restrict__ rnodes, const float4* __restrict__ prims,
-                                                 const f3 o, const f3 d) {
+// The node records are the child-pair table (bvh_ref_pairs: per node both children's boxes and references, 64 B):
+// a child's box is tested when its parent is processed, with the closest hit as of then — the t_max the reference
+// pushes it with and tests it against when it pops it — so only accepted nodes are pushed and visited, each with one
+// record load (round 6: the replay's share of C2 +1.0 % with the 32-B node records, a load per pushed node).
+__device__ __forceinline__ HitOut ref_trace_wave(const float4* __restrict__ rnodes, const float4* __restrict__ rpairs,
+                                                 const float4* __restrict__ prims, const f3 o, const f3 d) {
     int hit = -1;
     uint32_t tag = 0u;
     float t_best = FLT_MAX;
@@ -664,23 +669,24 @@ __device__ __forceinline__ HitOut ref_trace_wave(const float4* __restrict__ rnod
     float4 lo, hi;
     rec(rnodes, 0u, lo, hi);
     if (!ref_box(lo, hi, o, inv, FLT_MAX)) return HitOut{hit, tag, t_best};  // its own box first (Hittable.cuh:389)
-    uint32_t stk_n = 0u, stk_t = __float_as_uint(FLT_MAX);  // lane 0: the root, pushed with t_max = FLT_MAX
+    uint32_t stk_n = 0u;  // lane 0: the root (accepted)
     int top = 0;
     while (top >= 0) {
         const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)stk_n, top);
-        const float tm = __int_as_float(__builtin_amdgcn_readlane((int)stk_t, top));
         top--;
-        rec(rnodes, n, lo, hi);
-        if (!ref_box(lo, hi, o, inv, tm)) continue;
-        const int ch[2] = {__float_as_int(lo.w), __float_as_int(hi.w)};
+        float4 cl[2], ch[2];
+        rec(rpairs, 2u * n, cl[0], ch[0]);
+        rec(rpairs, 2u * n + 1u, cl[1], ch[1]);
         for (int k = 0; k < 2; k++) {
-            if (ch[k] >= 0) {
-                top++;
-                stk_n = lane_write(stk_n, (uint32_t)ch[k], (uint32_t)top);
-                stk_t = lane_write(stk_t, __float_as_uint(t_best), (uint32_t)top);
+            const int ref = __float_as_int(cl[k].w);
+            if (ref >= 0) {  // an inner node: pushed if its box accepts with t_max = the closest hit so far
+                if (ref_box(cl[k], ch[k], o, inv, t_best)) {
+                    top++;
+                    stk_n = lane_write(stk_n, (uint32_t)ref, (uint32_t)top);
+                }
                 continue;
             }
-            const uint32_t i = (uint32_t)~ch[k];  // PerformHit (Hittable.cuh:470-485) with t_max = the closest hit so far
+            const uint32_t i = (uint32_t)~ref;  // PerformHit (Hittable.cuh:470-485) with t_max = the closest hit so far
             float4 q0, q1;
             rec(prims, i, q0, q1);
             const uint32_t type = __float_as_uint(q1.w) & 15u;
@@ -1651,7 +1657,7 @@ __device__ __forceinline__ void bvh_replay_wave(PP P, const float4* __restrict__
         need &= need - 1u;
         const auto bl = [L](const float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L)); };
         const HitOut r = RT_BVH_EXACT == 4 ? HitOut{-1, 0u, 0.0f}
-                                           : ref_trace_wave(P->bvh_ref_nodes, prims, mk(bl(ro.x), bl(ro.y), bl(ro.z)),
+                                           : ref_trace_wave(P->bvh_ref_nodes, P->bvh_ref_pairs, prims, mk(bl(ro.x), bl(ro.y), bl(ro.z)),
                                                             mk(bl(rd.x), bl(rd.y), bl(rd.z)));
         if (__lane_id() == (uint32_t)L) {
             c.hit = RT_BVH_EXACT == 4 ? (c.hit >= 0 ? (c.hit | kVerifiedBit) : kVerifiedMiss)  // (A/B: no replay)
@@ -4276,6 +4282,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     KernelFn fn = pick(variant, count_tests, S.has_textures, philox, wide, g_wave_trace != nullptr);
     P.bvh_ref_nodes = (const float4*)S.bvh_ref_nodes;  // (the BVH kernels' exactness, bvh_clear)
     P.bvh_boxes = (const float4*)S.bvh_boxes;
+    P.bvh_ref_pairs = (const float4*)S.bvh_ref_pairs;
     P.bvh_has_rects = S.has_rects ? 1u : 0u;
     P.prefetch_stop = (uint32_t)g_prefetch_stop;
     if (V.kernel == 5 || V.kernel == 6) {  // the flat kernels' tables: primitives in the reference's test order, its BVH

@@ -84,6 +84,8 @@ struct HostScene {
     std::vector<float> bvh_ref_nodes;  // every scene: the reference BVH (ref_nodes' layout) with its primitive children
                                        // as ~(BVH-order index) — the BVH kernels' replay (render.hip bvh_clear)
     std::vector<float> bvh_boxes;      // ... and per BVH-order primitive its reference box: (lo.xyz, 0), (hi.xyz, 0)
+    std::vector<float> bvh_ref_pairs;  // ... and per reference node its two children: (lo.xyz, ref), (hi.xyz, 0) each
+                                       // (a primitive child's box is not used) — the wave-serial replay's records
 };
 
 // Validate + build (host only).  Returns RT_OK or an rt_status, with `err` set.  with_texels = false computes

@@ -19,6 +19,7 @@ struct DeviceScene {
     const void* flat_boxes = nullptr;  // per prims_flat record its reference box (exactness check), or NULL
     const void* bvh_ref_nodes = nullptr;  // the reference BVH over `prims` (BVH order), or NULL (bvh_clear, render.hip)
     const void* bvh_boxes = nullptr;      // per `prims` record its reference box, or NULL
+    const void* bvh_ref_pairs = nullptr;  // per reference node its children's boxes and references (ref_trace_wave)
     uint32_t flat_runs[2] = {0u, 0u};  // HostScene::flat_runs
     const void* mats = nullptr;    // float4 × 3 per material
     const void* imgs = nullptr;    // int4 per image

@@ -608,6 +608,22 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
                 o[4 * k + 3] = bits_to_float((uint32_t)enc);
             }
         }
+        // the same tree with each node's children's boxes in the node: (lo.xyz, ref), (hi.xyz, 0) per child, so the
+        // replay tests both children of a node from one 64-B record and visits only the nodes whose box accepted
+        out->bvh_ref_pairs.assign(rn.size() * 16, 0.0f);
+        for (size_t i = 0; i < rn.size(); i++) {
+            float* o = out->bvh_ref_pairs.data() + i * 16;
+            for (int k = 0; k < 2; k++) {
+                const int c = rn[i].child[k];
+                const int enc = c >= 0 ? c : ~bvh_index[~c];
+                if (c >= 0)
+                    for (int a = 0; a < 3; a++) {
+                        o[8 * k + a] = rn[c].lo[a];
+                        o[8 * k + 4 + a] = rn[c].hi[a];
+                    }
+                o[8 * k + 3] = bits_to_float((uint32_t)enc);
+            }
+        }
     }
     // Small scenes: the primitives once more, in the order the reference's own BVH tests them (the flat kernel,
     // render.hip, tests every primitive of every ray in this order, so its closest hit breaks exact ties in t as
