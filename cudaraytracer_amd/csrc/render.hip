@@ -3322,6 +3322,12 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
     }
     cnt.rays = rays;
     wave_pixels += queue.wave_pixels;
+#ifdef RT_LINGER_US
+    {  // (diagnostic A/B builds only: the wave stays resident, asleep, this long after its last pixel)
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 100u * (uint64_t)(RT_LINGER_US);
+        while (__builtin_amdgcn_s_memrealtime() < t_end) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
     trace_persistent_wave(P, queue, rt_start, wave_pixels);
     if constexpr (GROUP) {
