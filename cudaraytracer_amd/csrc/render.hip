@@ -271,6 +271,8 @@ struct KParams {
     uint32_t group_perm_a;           // GROUP: 0 = interleaved shares; else the shares' golden-ratio step (GroupShare)
     uint32_t group_perm_b, group_perm_k;  // ... (group_perm_k · group_perm_a) mod group_tiles, and tiles per share
     uint32_t queue_host_reset;       // persistent kernels: 1 = rt_render zeroed the queue slot (no queue_release)
+    uint32_t linger_ticks;           // persistent flat, GROUP: a finished workgroup waits at most this long (100 MHz
+                                     // ticks) for the grid's others before it exits (group_linger; 0: it does not)
     uint32_t group_chunk;            // ... positions per chunk (a multiple of 64)
 };
 
@@ -279,7 +281,10 @@ constexpr int kBlock = 256;
 // v4 work queue: the frame's work indices are split into this many contiguous ranges, each with its own
 // head 128 B from the next — one shared head serialises every wave's atomic in one L2 channel (≈ 16 ns
 // each: 0.5 ms for the 32400 chunks of a 1080p frame, the whole C5 frame time)
-constexpr uint32_t kQueueCounters = 16;  // <= 32: one word marks the exhausted heads (1-1024 heads measured)
+constexpr uint32_t kQueueCounters = 16;
+// A work-queue slot's words (each queue_stride apart): the heads, the exhausted-heads word, the finished count
+// (queue_release) and the arrived workgroups (group_linger)
+constexpr uint32_t kQueueSlotWords = kQueueCounters + 3;  // <= 32: one word marks the exhausted heads (1-1024 heads measured)
 static_assert(kQueueCounters >= 1 && kQueueCounters <= 32, "queue heads");
 constexpr uint32_t kQueueAllDone = kQueueCounters == 32 ? 0xffffffffu : (1u << kQueueCounters) - 1u;
 
@@ -2493,8 +2498,28 @@ __device__ __forceinline__ void queue_release(const KParams& P, const uint32_t a
     uint32_t fin = 0u;
     if (__lane_id() == leader) fin = atomicAdd(P.work_counter + (kQueueCounters + 1u) * P.queue_stride, 1u);
     fin = __builtin_amdgcn_readlane(fin, leader);
-    if (fin == arrivals - 1u && __lane_id() < kQueueCounters + 2u)
+    if (fin == arrivals - 1u && __lane_id() < kQueueSlotWords)
         __hip_atomic_store(P.work_counter + __lane_id() * P.queue_stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The end of a GROUP workgroup (wave 0, after a barrier the group's 16 waves all reached).  With P.linger_ticks
+// (RT_TUNE_GROUP_LINGER_US, off by default) the group stays resident — asleep, polling the count of arrived workgroups
+// — until every workgroup of the grid has finished its pixels, or the deadline passes, then leaves (queue_release
+// counts the leavers; the last zeroes the slot).  Measured (profiles/r06h_c5_linger.txt): waves that exit while others
+// still render stall those (a depth-1 frame's stragglers spent 24-84 us in their last pass), and with the finished
+// groups resident the stragglers run at full speed and every group leaves within ~1-4 us of the last pixel — but the
+// kernel then ends ~100 us after the groups leave together, where exits spread over the tail cost ~10 us: C5 0.23 ->
+// 0.31 ms.  The deadline bounds the wait when a workgroup of the grid is not resident, so every wave always exits.
+__device__ __forceinline__ void group_linger(const KParams& P) {
+    if (P.linger_ticks && !P.queue_host_reset && __lane_id() == 0) {
+        uint32_t* const arrived = P.work_counter + (kQueueCounters + 2u) * P.queue_stride;
+        atomicAdd(arrived, 1u);
+        const uint64_t deadline = __builtin_amdgcn_s_memrealtime() + P.linger_ticks;
+        while (__hip_atomic_load(arrived, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x &&
+               __builtin_amdgcn_s_memrealtime() < deadline)
+            __builtin_amdgcn_s_sleep(8);
+    }
+    queue_release(P, gridDim.x);
 }
 
 // Wave trace of the persistent kernels (rt_set_wave_trace; tools/v4_timeline.py), kWaveTraceWords words per wave:
@@ -3331,13 +3356,15 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
     cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
     trace_persistent_wave(P, queue, rt_start, wave_pixels);
     if constexpr (GROUP) {
-        // one device-scope arrival per workgroup, by its last wave (an LDS count): 4 096 waves ending within tens of
-        // microseconds serialised on the one finished-waves word (~12 ns each, MI355X_MICROARCH.md fan-in)
-        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
-        uint32_t fin = 0u;
-        if (__lane_id() == leader) fin = __hip_atomic_fetch_add(share_next + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        fin = __builtin_amdgcn_readlane(fin, leader);
-        if (fin == (blockDim.x >> 6) - 1u) queue_release(P, gridDim.x);
+        // the group's waves wait for each other at a barrier (asleep), then for the grid (group_linger), and leave
+        // together; one device-scope arrival per workgroup (4 096 waves ending within tens of microseconds serialised
+        // on the one finished-waves word, ~12 ns each, MI355X_MICROARCH.md fan-in)
+        __syncthreads();
+        if (threadIdx.x < 64u) group_linger(P);
+        __syncthreads();
+        // (wave trace: word 7, the queue-atomic wait of the per-wave queue, holds when the group left instead)
+        if (TRACE && P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (wave_id + 1ull) <= P.wave_trace_words)
+            P.wave_trace[(size_t)kWaveTraceWords * wave_id + 7] = __builtin_amdgcn_s_memrealtime();
     } else {
         queue_release(P, grid_waves());
     }
@@ -3509,6 +3536,8 @@ thread_local int g_group_tail = 0;
 thread_local int g_group_order = 0;
 // RT_TUNE_GROUP_CHUNK: positions per chunk of the workgroup chunk queue (RT_TUNE_PERSISTENT_GROUP 2)
 thread_local int g_group_chunk = 1024;
+// RT_TUNE_GROUP_LINGER_US: a finished workgroup waits up to this long for the grid's others before it exits (0: off)
+thread_local int g_group_linger_us = 0;
 // RT_TUNE_QUEUE_RESET: 1 = rt_render zeroes the persistent kernels' queue slot per launch (and they skip queue_release)
 thread_local int g_queue_host_reset = 0;
 template <bool PH, int G>
@@ -3717,7 +3746,7 @@ int acquire_queue(int device, uint32_t stride, uint32_t** head, int* cus) {
         return RT_ERR_DEVICE;
     }
     QueueRing& q = g_queues[device];
-    const size_t need = (size_t)(dev::kQueueCounters + 2u) * stride;
+    const size_t need = (size_t)dev::kQueueSlotWords * stride;
     std::lock_guard<std::mutex> lock(g_queue_mu);
     if (!q.buf || q.slot_bytes < need) {
         if (q.buf) {
@@ -3955,6 +3984,15 @@ int rt_set_tuning(int key, int value) {
         }
         int prev = g_prefetch_stop;
         g_prefetch_stop = value;
+        return prev;
+    }
+    if (key == RT_TUNE_GROUP_LINGER_US) {
+        if (value < 0 || value > 100000) {
+            set_error("rt_set_tuning: group linger must be in [0, 100000] us");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_group_linger_us;
+        g_group_linger_us = value;
         return prev;
     }
     if (key == RT_TUNE_GROUP_CHUNK) {
@@ -4331,6 +4369,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         const uint32_t tail_tiles =
             group && group_mode == 1 ? (uint32_t)(((uint64_t)tiles * (uint32_t)g_group_tail + 999u) / 1000u) : tiles;
         P.group_chunk = (uint32_t)g_group_chunk;
+        P.linger_ticks = group ? (uint32_t)g_group_linger_us * 100u : 0u;
         P.group_tiles = tiles - tail_tiles;
         P.queue_base = P.group_tiles * 64u;
         P.work_per_counter = (tail_tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
@@ -4361,7 +4400,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         // RT_TUNE_QUEUE_RESET asks for the round-4 host memset)
         P.queue_host_reset = g_queue_host_reset ? 1u : 0u;
         if (g_queue_host_reset) {
-            int rc2 = hip_check(hipMemsetAsync(P.work_counter, 0, (size_t)(dev::kQueueCounters + 2u) * P.queue_stride * 4u, s),
+            int rc2 = hip_check(hipMemsetAsync(P.work_counter, 0, (size_t)dev::kQueueSlotWords * P.queue_stride * 4u, s),
                                 "rt_render: queue reset");
             if (rc2 != RT_OK) return rc2;
         }
@@ -4391,7 +4430,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     // that the launch reusing it kQueueSlots launches later never finds exhausted heads (the slot is
     // otherwise clean only because the grid's last wave zeroes it in queue_release)
     if (rc != RT_OK && persistent)
-        (void)hipMemsetAsync(P.work_counter, 0, (size_t)(dev::kQueueCounters + 2u) * P.queue_stride * 4u, s);
+        (void)hipMemsetAsync(P.work_counter, 0, (size_t)dev::kQueueSlotWords * P.queue_stride * 4u, s);
     if (trial) (void)hipEventRecord(trial->ev[trial_slot + 1], s);  // the render kernel alone (v4 has no plan step)
     if (rc == RT_OK && plan) {  // the next launch on this stream dispatches this frame's costliest tiles first
         hipLaunchKernelGGL(dev::plan_order_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)plan->cost, plan->order,

@@ -412,7 +412,10 @@ int rt_last_variant(void);
  *   shares (0..1000, default 0).  RT_TUNE_GROUP_ORDER: the shares' tiles interleaved (0, default: tile g + k·groups) or in
  *   golden-ratio order (1: share g holds tiles (j · A) mod S, j in [g·K, g·K + K)).  None of these changes
  *   the image.  RT_TUNE_QUEUE_RESET: 1 = rt_render zeroes the persistent kernels' work-queue slot with a memset per
- *   launch; 0 (default) = the launch's last wave (GROUP: last workgroup) leaves it zeroed. */
+ *   launch; 0 (default) = the launch's last wave (GROUP: last workgroup) leaves it zeroed.  RT_TUNE_GROUP_LINGER_US: a
+ *   workgroup of the persistent flat kernel that has finished its pixels stays resident, asleep, until every workgroup
+ *   has (waves exiting while others render stall them), at most this long (0..100000; default 0 = exit at once: the
+ *   groups' simultaneous exit then costs the kernel's end ~100 us, more than the stall it avoids). */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
@@ -420,7 +423,8 @@ enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_
                      RT_TUNE_FLAT_MAX = 12, RT_TUNE_QUEUE_PREFETCH = 13, RT_TUNE_QUEUE_GUIDE = 14,
                      RT_TUNE_QUEUE_MIN_CHUNK = 15, RT_TUNE_RIUS_TRIPS_PERSISTENT = 16, RT_TUNE_PREFETCH_STOP = 17,
                      RT_TUNE_PERSISTENT_GROUP = 18, RT_TUNE_GROUP_TAIL = 19, RT_TUNE_GROUP_ORDER = 20,
-                     RT_TUNE_QUEUE_RESET = 21, RT_TUNE_GROUP_CHUNK = 22 };
+                     RT_TUNE_QUEUE_RESET = 21, RT_TUNE_GROUP_CHUNK = 22,
+                     RT_TUNE_GROUP_LINGER_US = 23 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */
