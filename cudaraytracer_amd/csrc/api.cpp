@@ -487,7 +487,8 @@ int rt_build_host_tables(const rt_scene_desc* desc, float* nodes, float* prims, 
     info->num_materials = h.num_mats;
     info->depth = h.depth;
     if (nodes) std::copy(h.nodes.begin(), h.nodes.end(), nodes);
-    if (prims) std::copy(h.prims.begin(), h.prims.end(), prims);
+    // (num_prims records: an empty scene's table carries one zero record for the device, not for the caller)
+    if (prims) std::copy(h.prims.begin(), h.prims.begin() + (size_t)h.num_prims * 8, prims);
     if (materials) std::copy(h.mats.begin(), h.mats.end(), materials);
     if (prim_source) std::copy(h.prim_source.begin(), h.prim_source.end(), prim_source);
     return RT_OK;
