@@ -3356,15 +3356,24 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
     cnt.primary = __lane_id() == 0 ? wave_pixels * P.spp : 0u;  // spp camera rays per pixel taken
     trace_persistent_wave(P, queue, rt_start, wave_pixels);
     if constexpr (GROUP) {
-        // the group's waves wait for each other at a barrier (asleep), then for the grid (group_linger), and leave
-        // together; one device-scope arrival per workgroup (4 096 waves ending within tens of microseconds serialised
-        // on the one finished-waves word, ~12 ns each, MI355X_MICROARCH.md fan-in)
-        __syncthreads();
-        if (threadIdx.x < 64u) group_linger(P);
-        __syncthreads();
-        // (wave trace: word 7, the queue-atomic wait of the per-wave queue, holds when the group left instead)
-        if (TRACE && P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (wave_id + 1ull) <= P.wave_trace_words)
-            P.wave_trace[(size_t)kWaveTraceWords * wave_id + 7] = __builtin_amdgcn_s_memrealtime();
+        // one device-scope arrival per workgroup (4 096 waves ending within tens of microseconds serialised on the one
+        // finished-waves word, ~12 ns each, MI355X_MICROARCH.md fan-in); with RT_TUNE_GROUP_LINGER_US the group's waves
+        // wait for each other at a barrier (asleep), then for the grid (group_linger), and leave together
+        if (P.linger_ticks) {  // (launch-uniform: every wave of the group takes the same branch)
+            __syncthreads();
+            if (threadIdx.x < 64u) group_linger(P);
+            __syncthreads();
+            // (wave trace: word 7, the queue-atomic wait of the per-wave queue, holds when the group left instead)
+            if (TRACE && P.wave_trace && wave_leader() && (uint64_t)kWaveTraceWords * (wave_id + 1ull) <= P.wave_trace_words)
+                P.wave_trace[(size_t)kWaveTraceWords * wave_id + 7] = __builtin_amdgcn_s_memrealtime();
+        } else {  // each wave exits when its lanes are done; the group's last wave (an LDS count) releases the slot
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+            uint32_t fin = 0u;
+            if (__lane_id() == leader)
+                fin = __hip_atomic_fetch_add(share_next + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            fin = __builtin_amdgcn_readlane(fin, leader);
+            if (fin == (blockDim.x >> 6) - 1u) queue_release(P, gridDim.x);
+        }
     } else {
         queue_release(P, grid_waves());
     }
