@@ -39,6 +39,7 @@ RT_TUNE_GROUP_ORDER = 20  # ... the shares' tiles interleaved (0) or in golden-r
 RT_TUNE_QUEUE_RESET = 21  # 1 = rt_render memsets the persistent queue slot per launch
 RT_TUNE_GROUP_CHUNK = 22  # ... positions per chunk of the workgroup chunk queue (group mode 2)
 RT_TUNE_GROUP_LINGER_US = 23  # ... a finished workgroup waits this long (us) for the grid's others before exiting
+RT_TUNE_GROUP_WAVES = 24  # ... waves per workgroup of the persistent flat kernel's group builds (4/8/12/16)
 RT_TUNE_GROUP_TAIL = 19  # ... permille of the tiles left to the per-wave queue behind the shares
 
 STATUS = {

@@ -3545,6 +3545,8 @@ thread_local int g_group_tail = 0;
 thread_local int g_group_order = 0;
 // RT_TUNE_GROUP_CHUNK: positions per chunk of the workgroup chunk queue (RT_TUNE_PERSISTENT_GROUP 2)
 thread_local int g_group_chunk = 1024;
+// RT_TUNE_GROUP_WAVES: waves per workgroup of the GROUP builds (4, 8, 12 or 16)
+thread_local int g_group_waves = 16;
 // RT_TUNE_GROUP_LINGER_US: a finished workgroup waits up to this long for the grid's others before it exits (0: off)
 thread_local int g_group_linger_us = 0;
 // RT_TUNE_QUEUE_RESET: 1 = rt_render zeroes the persistent kernels' queue slot per launch (and they skip queue_release)
@@ -3995,6 +3997,15 @@ int rt_set_tuning(int key, int value) {
         g_prefetch_stop = value;
         return prev;
     }
+    if (key == RT_TUNE_GROUP_WAVES) {
+        if (value < 4 || value > 16 || value % 4) {
+            set_error("rt_set_tuning: group waves must be 4, 8, 12 or 16");
+            return RT_ERR_INVALID_ARGUMENT;
+        }
+        int prev = g_group_waves;
+        g_group_waves = value;
+        return prev;
+    }
     if (key == RT_TUNE_GROUP_LINGER_US) {
         if (value < 0 || value > 100000) {
             set_error("rt_set_tuning: group linger must be in [0, 100000] us");
@@ -4325,7 +4336,9 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     P.lds_wave_words = (uint32_t)(wave_bytes / 4);
     // the persistent flat kernel's GROUP build: 16-wave workgroups (one per CU) whose share counter follows the tables
     const bool group = V.kernel == 6 && g_persistent_group != 0;
-    const uint32_t block = group ? 1024u : (uint32_t)V.block;
+    const uint32_t block = group ? (uint32_t)g_group_waves * 64u : (uint32_t)V.block;
+    // GROUP: the workgroups per CU the grid is sized for (kFlatPersistentWaves waves per SIMD, e.g. 1 of 16 waves)
+    const int group_per_cu = std::max(1, kFlatPersistentWaves * 4 / std::max(1, g_group_waves));
     size_t lds_bytes = (V.stack == dev::STACK_LDS ? (size_t)V.lds_depth * V.block * 4 : 0) + wave_bytes +
                        (V.kernel == 6 ? flat_tab_bytes + (group ? 4u * (2u + dev::kGqWords) : 0u) : 0);  // (GROUP)
     if (lds_bytes > kLdsLimit) {
@@ -4360,10 +4373,10 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
             rc = hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, block, lds_bytes),
                            "rt_render: occupancy query");
         if (rc != RT_OK) return rc;
-        if (group && per_cu > 1) {
-            // two 16-wave groups would fit a CU by registers: claim over half the CU's LDS so that the 1-per-CU grid
-            // below cannot put two groups on one CU and leave another empty
-            lds_bytes = std::max(lds_bytes, kLdsLimit / 2u + 1024u);
+        if (group && per_cu > group_per_cu) {
+            // more groups would fit a CU by registers than the grid is sized for: claim enough of the CU's LDS that
+            // the grid cannot put more on one CU and leave another short
+            lds_bytes = std::max(lds_bytes, kLdsLimit / (size_t)(group_per_cu + 1) + 1024u);
             rc = hip_check(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes),
                            "rt_render: LDS size attribute");
             if (rc != RT_OK) return rc;
@@ -4384,7 +4397,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
         P.work_per_counter = (tail_tiles + dev::kQueueCounters - 1u) / dev::kQueueCounters * 64u;
         // the persistent flat kernel runs 4 waves per SIMD even where its registers allow 5-6: C5 0.294 vs 0.307 ms
         // (XORWOW), 0.300 vs 0.314 (Philox), 3 rounds on one box (profiles/r04f_ab_pflat_waves.txt)
-        if (V.kernel == 6) per_cu = std::min(per_cu, std::max(1, kFlatPersistentWaves * 4 * 64 / (int)block));
+        if (V.kernel == 6) per_cu = std::min(per_cu, group ? group_per_cu : std::max(1, kFlatPersistentWaves * 4 * 64 / (int)block));
         if (g_persistent_waves > 0) per_cu = std::max(1, g_persistent_waves * 4 * 64 / (int)block);
         const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
         if (group) grid = (tiles + block / 64u - 1u) / (block / 64u);  // (no more waves than tiles, as one-wave grids)

@@ -415,7 +415,9 @@ int rt_last_variant(void);
  *   launch; 0 (default) = the launch's last wave (GROUP: last workgroup) leaves it zeroed.  RT_TUNE_GROUP_LINGER_US: a
  *   workgroup of the persistent flat kernel that has finished its pixels stays resident, asleep, until every workgroup
  *   has (waves exiting while others render stall them), at most this long (0..100000; default 0 = exit at once: the
- *   groups' simultaneous exit then costs the kernel's end ~100 us, more than the stall it avoids). */
+ *   groups' simultaneous exit then costs the kernel's end ~100 us, more than the stall it avoids).
+ *   RT_TUNE_GROUP_WAVES: waves per workgroup of those builds (4, 8, 12 or 16, default 16; the grid keeps 4 waves per
+ *   SIMD where the group size divides 16, else the one group per CU that fits). */
 enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_PERSISTENT_WAVES = 2,
                      RT_TUNE_SAH_TRAVERSAL = 3, RT_TUNE_LDS_PAD = 4, RT_TUNE_ADAPTIVE_ORDER = 5,
                      RT_TUNE_TEXEL_LAYOUT = 6, RT_TUNE_QUEUE_CHUNK = 7, RT_TUNE_QUEUE_STRIDE = 8,
@@ -424,7 +426,7 @@ enum rt_tuning_key { RT_TUNE_REGEN_THRESHOLD = 0, RT_TUNE_LEAF_MAX = 1, RT_TUNE_
                      RT_TUNE_QUEUE_MIN_CHUNK = 15, RT_TUNE_RIUS_TRIPS_PERSISTENT = 16, RT_TUNE_PREFETCH_STOP = 17,
                      RT_TUNE_PERSISTENT_GROUP = 18, RT_TUNE_GROUP_TAIL = 19, RT_TUNE_GROUP_ORDER = 20,
                      RT_TUNE_QUEUE_RESET = 21, RT_TUNE_GROUP_CHUNK = 22,
-                     RT_TUNE_GROUP_LINGER_US = 23 };
+                     RT_TUNE_GROUP_LINGER_US = 23, RT_TUNE_GROUP_WAVES = 24 };
 int rt_set_tuning(int key, int value);
 
 /* ------------------------------------------------------------------------------------------------ */

@@ -1089,3 +1089,29 @@ def test_persistent_flat_group_queue_chunks(chunk):
         lib().rt_set_variant(-1)
         for k, v in zip(keys, prev):
             lib().rt_set_tuning(k, v)
+
+
+@pytest.mark.parametrize("waves, group", [(4, 2), (8, 2), (12, 2), (12, 1)])
+def test_persistent_flat_group_sizes(waves, group):
+    """Workgroups of 4, 8 or 12 waves instead of 16 (RT_TUNE_GROUP_WAVES), with the chunk queue and with static shares:
+    the golden image, rays and RNG states."""
+    keys = (abi.RT_TUNE_PERSISTENT_GROUP, abi.RT_TUNE_GROUP_WAVES)
+    prev = [lib().rt_set_tuning(k, v) for k, v in zip(keys, (group, waves))]
+    assert min(prev) >= 0
+    lib().rt_set_variant(6)
+    try:
+        for name in ("c5_textured_160x96_s4", "c3_cornell_128_s16"):
+            case = CASE_BY_NAME[name]
+            cfg, g = case.cfg(), load_golden(case.name)
+            r = Renderer(cfg.width, cfg.height)
+            r.render_init()
+            r.render(DeviceScene(scenes.builtin(cfg.scene)), cfg.spp, cfg.depth, cfg.inputs(), flags=case.flags)
+            torch.cuda.synchronize()
+            assert lib().rt_last_variant() == 6
+            np.testing.assert_array_equal(r.image(), g["pos"], err_msg=name)
+            assert digest(r.states()[:, :6]) == g["state_after_sha256"].tobytes(), name
+            assert int(r.counters[0]) == int(g["counters"][0]), name
+    finally:
+        lib().rt_set_variant(-1)
+        for k, v in zip(keys, prev):
+            lib().rt_set_tuning(k, v)
