@@ -64,7 +64,8 @@ static void free_device(DeviceScene* s) {
     if (s->prims_flat) (void)hipFree((void*)s->prims_flat);
     if (s->ref_nodes) (void)hipFree((void*)s->ref_nodes);
     if (s->flat_boxes) (void)hipFree((void*)s->flat_boxes);
-    s->prims_flat = s->ref_nodes = s->flat_boxes = nullptr;
+    if (s->flat_ref_pairs) (void)hipFree((void*)s->flat_ref_pairs);
+    s->prims_flat = s->ref_nodes = s->flat_boxes = s->flat_ref_pairs = nullptr;
     if (s->bvh_ref_nodes) (void)hipFree((void*)s->bvh_ref_nodes);
     if (s->bvh_boxes) (void)hipFree((void*)s->bvh_boxes);
     if (s->bvh_ref_pairs) (void)hipFree((void*)s->bvh_ref_pairs);
@@ -96,6 +97,8 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.prims_flat = p;
     if ((rc = upload(h.ref_nodes, &p, "hipMalloc/hipMemcpy(ref_nodes)"))) goto fail;
     d.ref_nodes = p;
+    if ((rc = upload(h.flat_ref_pairs, &p, "hipMalloc/hipMemcpy(flat_ref_pairs)"))) goto fail;
+    d.flat_ref_pairs = p;
     if ((rc = upload(h.flat_boxes, &p, "hipMalloc/hipMemcpy(flat_boxes)"))) goto fail;
     d.flat_boxes = p;
     if ((rc = upload(h.bvh_ref_nodes, &p, "hipMalloc/hipMemcpy(bvh_ref_nodes)"))) goto fail;
@@ -126,7 +129,7 @@ int create_device_scene(const HostScene& h, rt_scene** out, std::shared_ptr<void
     d.has_textures = h.has_textures;
     d.has_rects = h.has_rects;
     d.device_bytes = (h.nodes.size() + h.nodes48.size() + h.refs.size() + h.prims.size() + h.prims_flat.size() + h.ref_nodes.size() +
-                      h.flat_boxes.size() + h.bvh_ref_nodes.size() + h.bvh_boxes.size() + h.bvh_ref_pairs.size() + h.mats.size()) * 4 +
+                      h.flat_boxes.size() + h.flat_ref_pairs.size() + h.bvh_ref_nodes.size() + h.bvh_boxes.size() + h.bvh_ref_pairs.size() + h.mats.size()) * 4 +
                      h.imgs.size() * 4 + h.texels.size();
     *out = s;
     return RT_OK;

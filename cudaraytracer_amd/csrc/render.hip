@@ -258,7 +258,8 @@ struct KParams {
     uint32_t regen_live_frac;        // v3: threshold cap as a fraction of the wave's live pixels (x/64; 0 = off)
     uint32_t leaf_break;             // v3: leave the node loop once at most this many lanes still lack a leaf
     uint32_t rius_cap;               // flat: RandomInUnitSphere attempts per shading pass (0xffffffff = unbounded)
-    const float4* ref_nodes;         // flat kernel: the reference BVH over the flat table (ref_trace)
+    const float4* ref_nodes;         // flat kernel: the reference BVH over the flat table (ref_trace_wave's root box)
+    const float4* flat_ref_pairs;    // flat kernel: the same tree as child-pair records (ref_trace_wave)
     const float4* flat_boxes;        // flat kernel: per flat record its reference box (flat_trace's exactness check)
     uint32_t flat_runs[2];           // flat kernel: [begin, end) of each primitive type's run in the flat table
     const float4* bvh_ref_nodes;     // BVH kernels: the reference BVH over `prims` (bvh_clear), NULL = no replay
@@ -450,8 +451,8 @@ __device__ __forceinline__ int trace(const float4* __restrict__ nodes, const flo
 // The reference's own closest-hit query, replayed exactly: BVHNode::Hit (Hittable.cuh:387-439) over the tree the
 // BVHNode constructor builds (ref_nodes, scene_build.cpp), with AABB::Hit (AABB.cuh:30-50) on the reference's boxes and
 // its t_max bookkeeping (a node's box is tested against the closest hit as of its push).  Per lane, with a private
-// stack: the flat kernel runs it only for the rare rays whose answer box culling could change (flat_trace).
-constexpr int kRefStack = 16;     // > kRefTreeMaxDepth (rt_internal.h): the flat kernels' replay
+// stack: the v1/v2 kernels call it for the rare rays whose answer box culling could change (bvh_replay); since round 6
+// the v3/v4 and flat kernels replay wave-serially instead (ref_trace_wave), without a call or private memory.
 constexpr int kRefStackBvh = 32;  // > kRefTreeMaxDepthBvh: the BVH kernels' (bvh_clear)
 __device__ __forceinline__ bool ref_box(const float4 lo, const float4 hi, const f3 o, const f3 inv, float t_max) {
     float t_min = kTmin;
@@ -659,8 +660,11 @@ __device__ __forceinline__ uint32_t lane_write(uint32_t vec, const uint32_t val,
 // a child's box is tested when its parent is processed, with the closest hit as of then — the t_max the reference
 // pushes it with and tests it against when it pops it — so only accepted nodes are pushed and visited, each with one
 // record load (round 6: the replay's share of C2 +1.0 % with the 32-B node records, a load per pushed node).
+// lstk (the flat kernels): the stack in this wave's LDS words instead of VGPR lanes — a partial tile's flat kernel
+// wave has inactive lanes, which a lane stack cannot use.
 __device__ __forceinline__ HitOut ref_trace_wave(const float4* __restrict__ rnodes, const float4* __restrict__ rpairs,
-                                                 const float4* __restrict__ prims, const f3 o, const f3 d) {
+                                                 const float4* __restrict__ prims, const f3 o, const f3 d,
+                                                 uint32_t* lstk = nullptr) {
     int hit = -1;
     uint32_t tag = 0u;
     float t_best = FLT_MAX;
@@ -675,9 +679,11 @@ __device__ __forceinline__ HitOut ref_trace_wave(const float4* __restrict__ rnod
     rec(rnodes, 0u, lo, hi);
     if (!ref_box(lo, hi, o, inv, FLT_MAX)) return HitOut{hit, tag, t_best};  // its own box first (Hittable.cuh:389)
     uint32_t stk_n = 0u;  // lane 0: the root (accepted)
+    if (lstk) lstk[0] = 0u;
     int top = 0;
     while (top >= 0) {
-        const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)stk_n, top);
+        const uint32_t n = lstk ? (uint32_t)__builtin_amdgcn_readfirstlane((int)lstk[top])
+                                : (uint32_t)__builtin_amdgcn_readlane((int)stk_n, top);
         top--;
         float4 cl[2], ch[2];
         rec(rpairs, 2u * n, cl[0], ch[0]);
@@ -687,7 +693,8 @@ __device__ __forceinline__ HitOut ref_trace_wave(const float4* __restrict__ rnod
             if (ref >= 0) {  // an inner node: pushed if its box accepts with t_max = the closest hit so far
                 if (ref_box(cl[k], ch[k], o, inv, t_best)) {
                     top++;
-                    stk_n = lane_write(stk_n, (uint32_t)ref, (uint32_t)top);
+                    if (lstk) lstk[top] = (uint32_t)ref;
+                    else stk_n = lane_write(stk_n, (uint32_t)ref, (uint32_t)top);
                 }
                 continue;
             }
@@ -2682,7 +2689,7 @@ template <bool COUNT_TESTS>
 __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, const float4* __restrict__ rnodes,
                                            const float4* __restrict__ boxes, const uint32_t n, const uint32_t runs0,
                                            const uint32_t runs1, const f3 ro, const f3 rd, int& hit, uint32_t& tag,
-                                           float& t_best, Counts& cnt) {
+                                           float& t_best, Counts& cnt, bool& replay) {
     hit = -1;
     tag = 0u;
     t_best = FLT_MAX;
@@ -2813,12 +2820,31 @@ __device__ __forceinline__ void flat_trace(const float4* __restrict__ prims, con
         }
     }
     const bool tie = (tie_m >> __lane_id()) & 1u;
-    if (tie || nan || edge || t_best != t_best) {
-        if (COUNT_TESTS) cnt.replays++;
-        const HitOut r = ref_trace<kRefStack>(rnodes, prims, ro, rd);
-        hit = r.hit;
-        tag = r.tag;
-        t_best = r.t;
+    // such a ray replays the reference traversal at the top of the next pass, where every lane of the wave is active
+    // (flat_replay_wave: wave-serial, no call, no private stack; round 5's called ref_trace with its 16-entry private
+    // stack cost C3 10.6 % and C5 3.8 % through the call's register convention in the hot loop, not its ~1e-5 replays)
+    replay = tie || nan || edge || t_best != t_best;
+    if (COUNT_TESTS && replay) cnt.replays++;
+}
+
+// The flat kernels' lanes in MODE_REPLAY (flat_trace flagged their closest hit), one after another through
+// ref_trace_wave over the reference tree of the flat table; each gets the reference's answer and shades it (MODE_SHADE).
+// Its stack is in LDS (lstk, 32 words per wave): a partial tile's wave has inactive lanes.
+__device__ __forceinline__ void flat_replay_wave(KParamsC* q, uint32_t* lstk, int& mode, int& hit, uint32_t& tag,
+                                                 float& t, const f3 ro, const f3 rd) {
+    uint64_t need = __ballot(mode == MODE_REPLAY);
+    while (need != 0u) {
+        const int L = (int)__builtin_ctzll(need);
+        need &= need - 1u;
+        const auto bl = [L](const float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L)); };
+        const HitOut r = ref_trace_wave(q->ref_nodes, q->flat_ref_pairs, q->prims, mk(bl(ro.x), bl(ro.y), bl(ro.z)),
+                                        mk(bl(rd.x), bl(rd.y), bl(rd.z)), lstk);
+        if (__lane_id() == (uint32_t)L) {
+            hit = r.hit;
+            tag = r.tag;
+            t = r.t;
+            mode = MODE_SHADE;
+        }
     }
 }
 
@@ -2832,6 +2858,7 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
     const uint32_t tile = (P.tile_order && slot < P.num_tiles) ? P.tile_order[slot] : slot;
     if (!lane_pixel<64>(P, x, g, pix, tile)) return;
     const bool rtl = P.rius_rtl != 0;
+    __shared__ uint32_t replay_stk[32];  // flat_replay_wave's stack (one wave per workgroup)
     uint32_t* st = state_at(P, pix);
     R rng = begin_rng<R>(st, P.state_stride, g * P.width + x);  // global pixel index (Kernel.cu:119)
 
@@ -2900,13 +2927,17 @@ __global__ __launch_bounds__(64, WAVES_PER_SIMD) void render_kernel_flat(const K
             cnt.idle_nt += lead * (uint32_t)__popcll(__ballot(mode == MODE_TRAV));
             cnt.idle_fin += lead * (uint32_t)__popcll(__ballot(mode == MODE_TRAV || mode == MODE_SHADE));
         }
+        // flat_trace flagged these lanes' closest hits last pass: the reference traversal, then they shade below
+        if (__builtin_expect(__ballot(mode == MODE_REPLAY) != 0u, 0))
+            flat_replay_wave(kparams_reload(), replay_stk, mode, hit, tag, t, ro, rd);
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
             // the scan's launch-uniform operands re-read per pass (as the persistent flat kernel's)
             KParamsC* const q = kparams_reload();
+            bool replay;
             flat_trace<COUNT_TESTS>(q->prims, q->ref_nodes, q->flat_boxes, q->num_prims, q->flat_runs[0], q->flat_runs[1], ro,
-                                    rd, hit, tag, t, cnt);
-            mode = MODE_SHADE;
+                                    rd, hit, tag, t, cnt, replay);
+            mode = replay ? MODE_REPLAY : MODE_SHADE;
         }
         const uint64_t c1 = COUNT_TESTS ? __builtin_amdgcn_s_memtime() : 0;
         if (COUNT_TESTS) cnt.ctrav += c1 - c0;
@@ -3177,6 +3208,7 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
     float4* const tboxes = tprims + 2u * P.num_prims;
     float4* const tmats = tboxes + 2u * P.num_prims;
     int4* const timgs = reinterpret_cast<int4*>(tmats + 3u * P.num_mats);
+    __shared__ uint32_t replay_stk[(GROUP ? 16 : 1) * 32];  // flat_replay_wave's stacks, 32 words per wave
     // GROUP: the share's LDS counter after the tables (rt_render sizes the LDS for it)
     uint32_t* const share_next = reinterpret_cast<uint32_t*>(timgs + P.num_imgs);
     {
@@ -3237,14 +3269,18 @@ __global__ __launch_bounds__(GROUP ? 1024 : 64, WAVES_PER_SIMD) void render_kern
         const auto pass_stamp = [&](uint32_t k) {
             if (pass_traced && 4u * pass_no < kPassTrace && wave_leader()) pass_rec[4u * pass_no + k] = __builtin_amdgcn_s_memrealtime();
         };
+        // flat_trace flagged these lanes' closest hits last pass: the reference traversal, then they shade below
+        if (__builtin_expect(__ballot(mode == MODE_REPLAY) != 0u, 0))
+            flat_replay_wave(kparams_reload(), replay_stk + 32u * (threadIdx.x >> 6), mode, hit, tag, t, ro, rd);
         if (mode == MODE_TRAV) {  // (a lane resuming its RandomInUnitSphere call keeps its hit)
             rays++;
             // the scan's launch-uniform operands re-read per pass (s_load): hoisted out of the loop, the per-run
             // pointers, counts and masks derived from them overflowed the SGPR budget into VGPR-lane spills
             KParamsC* const q = kparams_reload();
+            bool replay;
             flat_trace<COUNT_TESTS>(q->prims, q->ref_nodes, tboxes, q->num_prims, q->flat_runs[0], q->flat_runs[1], ro, rd,
-                                    hit, tag, t, cnt);
-            mode = MODE_SHADE;
+                                    hit, tag, t, cnt, replay);
+            mode = replay ? MODE_REPLAY : MODE_SHADE;
         }
         pass_stamp(1);
         bool cam = false;
@@ -4354,6 +4390,7 @@ int rt_render(const rt_scene* scene, const rt_render_args* a, rt_stream stream) 
     if (V.kernel == 5 || V.kernel == 6) {  // the flat kernels' tables: primitives in the reference's test order, its BVH
         P.prims = (const float4*)S.prims_flat;
         P.ref_nodes = (const float4*)S.ref_nodes;
+        P.flat_ref_pairs = (const float4*)S.flat_ref_pairs;
         P.flat_boxes = (const float4*)S.flat_boxes;
         P.flat_runs[0] = S.flat_runs[0];
         P.flat_runs[1] = S.flat_runs[1];

@@ -77,6 +77,7 @@ struct HostScene {
     std::vector<float> prims_flat;     // scenes of <= kFlatMaxPrims primitives: the records in the reference BVH's
                                        // test order (the flat kernel's table), else empty
     std::vector<float> ref_nodes;      // ... and the reference BVH itself: 8 floats per node (scene_build.cpp)
+    std::vector<float> flat_ref_pairs; // ... and the same tree as child-pair records (16 floats per node)
     std::vector<float> flat_boxes;     // ... and per flat record its reference box for the flat kernels' exactness
                                        // check: 8 floats (scene_build.cpp)
     uint32_t flat_runs[2] = {0u, 0u};  // prims_flat holds each primitive type as one contiguous run: [begin, end) of

@@ -16,6 +16,7 @@ struct DeviceScene {
     const void* prims = nullptr;   // float4 × 2 per primitive
     const void* prims_flat = nullptr;  // the same records in the reference BVH's test order (small scenes), or NULL
     const void* ref_nodes = nullptr;   // the reference BVH (boxes + shape) over prims_flat, or NULL
+    const void* flat_ref_pairs = nullptr;  // ... as child-pair records (the flat kernels' wave-serial replay)
     const void* flat_boxes = nullptr;  // per prims_flat record its reference box (exactness check), or NULL
     const void* bvh_ref_nodes = nullptr;  // the reference BVH over `prims` (BVH order), or NULL (bvh_clear, render.hip)
     const void* bvh_boxes = nullptr;      // per `prims` record its reference box, or NULL

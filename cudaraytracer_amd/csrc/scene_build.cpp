@@ -677,6 +677,21 @@ int build_host_scene(const rt_scene_desc* desc, HostScene* out, std::string* err
                     o[4 * k + 3] = bits_to_float((uint32_t)enc);
                 }
             }
+            // ... and as child-pair records (bvh_ref_pairs' layout) for the wave-serial replay (ref_trace_wave)
+            out->flat_ref_pairs.assign(rn.size() * 16, 0.0f);
+            for (size_t i = 0; i < rn.size(); i++) {
+                float* o = out->flat_ref_pairs.data() + i * 16;
+                for (int k = 0; k < 2; k++) {
+                    const int c = rn[i].child[k];
+                    const int enc = c >= 0 ? c : ~flat_index[~c];
+                    if (c >= 0)
+                        for (int a = 0; a < 3; a++) {
+                            o[8 * k + a] = rn[c].lo[a];
+                            o[8 * k + 4 + a] = rn[c].hi[a];
+                        }
+                    o[8 * k + 3] = bits_to_float((uint32_t)enc);
+                }
+            }
         }
     }
     return RT_OK;
